@@ -1,0 +1,181 @@
+/*
+ * srt_amd.h -- C ABI of the MI355X-native path-tracing inner loop.
+ *
+ * Drop-in boundary for matteobir12/simple-ray-tracer's GL compute path.  The
+ * reference has no plugin system: its boundary is the GL program + uniform +
+ * binding contract that src/main.cpp drives every frame.  Each entry point
+ * below names the reference interface it replaces (file:line).  Plain
+ * pointers and sizes only; status codes instead of std::terminate /
+ * std::runtime_error.  Everything runs on one HIP stream per context.
+ */
+#ifndef SRT_AMD_H
+#define SRT_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRT_ABI_VERSION 1
+
+/* ---- status codes ---- */
+enum {
+  SRT_OK = 0,
+  SRT_ERR_INVALID = 1,    /* bad argument / size mismatch */
+  SRT_ERR_HIP = 2,        /* HIP runtime error (message: srt_last_error) */
+  SRT_ERR_NOT_FOUND = 3,  /* unknown uniform name (reference: silently ignored) */
+  SRT_ERR_IO = 4,         /* file open / parse failure */
+  SRT_ERR_STATE = 5,      /* missing scene / noise / images before dispatch */
+  SRT_ERR_LIMIT = 6       /* BVH deeper than the traversal stack supports */
+};
+
+/* ---- std430 records: the reference's SSBO / texel-buffer contents ----
+ * These are the host structs AssetUtils::UploadModelDataToGPU packs
+ * (src/asset_utils/gpu_loader.cpp:11-41) and the GLSL declares
+ * (shaders/raytrace_types.glsl:19-107).  The library re-lays them on device. */
+typedef struct { uint32_t first_index, count, pad0, pad1; float frame[16]; } srt_bvh_record;   /* 80 B, frame column-major (glm::mat4) */
+typedef struct { float min_bounds[3]; uint32_t first_child_or_prim_index;
+                 float max_bounds[3]; uint32_t prim_count; } srt_bvh_node;                    /* 32 B */
+typedef struct { float diffuse[3]; float specular_ex; float specular[3]; uint32_t use_texture;
+                 uint32_t handle[2]; uint32_t pad0, pad1; } srt_material_obj;                  /* 48 B */
+typedef struct { uint32_t v0_idx, v1_idx, v2_idx, material_idx; } srt_triangle;                 /* 16 B */
+typedef struct { float vertex[3]; float pad0; float texture[2]; float pad1[2]; } srt_vertex;    /* 32 B */
+typedef struct { float position[3]; float intensity; float color[3]; float pad1; } srt_light;  /* 32 B, raytracer/light.h:54-63 */
+typedef struct { float origin[3]; float pad0; float direction[3]; float intersection_distance; } srt_ray; /* 32 B, common/types.h:15-35 */
+
+/* Work counters of a counting launch. */
+typedef struct {
+  uint64_t rays;        /* CheckHit queries: camera + bounce + shadow */
+  uint64_t nodes;       /* BVH node box tests (32 B each) */
+  uint64_t tris;        /* triangle tests (40 B each) */
+  uint64_t rng_u;       /* noiseUniformTex fetches (4 B) */
+  uint64_t rng_sq;      /* noiseTex .xy fetches (8 B) */
+  uint64_t light_reads; /* light records (32 B) */
+  uint64_t mat_reads;   /* mesh material fetches (48 B) */
+  uint64_t samples;     /* path samples */
+  uint64_t stack_overflow;
+  uint64_t max_stack;
+} srt_stats;
+
+typedef struct srt_context srt_context;
+typedef struct srt_model srt_model;
+typedef struct srt_scene srt_scene;
+
+const char* srt_last_error(void);
+int srt_abi_version(void);
+
+/* ===================== Graphics::Compute (the dispatch API) =====================
+ * replaces Graphics::Compute(path) + Init() (include/graphics/shader.h:46-55,
+ * src/graphics/Shader.cpp:14-26,125-157) and Compute::CreateComputeProgram
+ * (include/compute/create_compute_program.h:46-72).  `stream` is a
+ * hipStream_t (NULL = the context creates its own). */
+int srt_create(int device, void* stream, srt_context** out);
+int srt_destroy(srt_context* ctx);
+void* srt_stream(srt_context* ctx);
+
+/* Uniform setters (Shader.cpp:79-122,159-212): names are the GLSL uniforms
+ * resetAccumBuffer, showModel (bool); Width, Height, accumFrames, lightCount,
+ * maxDepth (int); bvh_count (uint); cameraOrigin, cameraDirection,
+ * cameraUp, cameraRight (vec3).  Unknown name -> SRT_ERR_NOT_FOUND (the
+ * reference silently ignores it: callers may too). */
+int srt_set_bool(srt_context* ctx, const char* name, int v);
+int srt_set_int(srt_context* ctx, const char* name, int v);
+int srt_set_uint(srt_context* ctx, const char* name, uint32_t v);
+int srt_set_float(srt_context* ctx, const char* name, float v);
+int srt_set_vec3(srt_context* ctx, const char* name, float x, float y, float z);
+
+/* glDispatchCompute(gx, gy, 1) of raytrace_compute.glsl (src/main.cpp:706):
+ * one 8x8 invocation tile per group, one path sample per pixel. */
+int srt_dispatch(srt_context* ctx, uint32_t groups_x, uint32_t groups_y);
+/* glMemoryBarrier + glFinish (src/main.cpp:709-718). */
+int srt_finish(srt_context* ctx);
+
+/* Fused progressive render: equivalent to `nframes` consecutive dispatches
+ * with accumFrames = frame_first .. frame_first+nframes-1 and
+ * resetAccumBuffer = false (bit-identical accum buffer); the RGBA8 image is
+ * written once, for the last frame, when write_output != 0.  Counting
+ * launches (count != 0) also fill srt_get_stats. */
+int srt_render_frames(srt_context* ctx, int frame_first, int nframes, int write_output, int count);
+int srt_get_stats(srt_context* ctx, srt_stats* out);
+int srt_reset_stats(srt_context* ctx);
+
+/* Row-band sharding for multi-GPU: this context owns bands b of `band_rows`
+ * rows with b % nranks == rank; its images hold only those rows, packed in
+ * band order.  Default: rank 0 of 1 (whole frame). */
+int srt_set_tiling(srt_context* ctx, int rank, int nranks, int band_rows);
+int srt_local_rows(srt_context* ctx);
+
+/* ===================== bindings (SSBOs / texel buffers / images) ===================== */
+/* AssetUtils::UploadModelDataToGPU (include/asset_utils/gpu_loader.h:19,
+ * src/asset_utils/gpu_loader.cpp:63-183): the five SSBOs at bindings 5..9.
+ * tex_albedo: 3 floats per material = the texture() result for use_texture
+ * materials (may be NULL when none use textures). */
+int srt_upload_scene(srt_context* ctx,
+                     const srt_bvh_record* bvhs, uint32_t n_bvhs,
+                     const srt_bvh_node* nodes, uint32_t n_nodes,
+                     const srt_material_obj* mats, const float* tex_albedo, uint32_t n_mats,
+                     const srt_triangle* tris, uint32_t n_tris,
+                     const srt_vertex* verts, uint32_t n_verts);
+/* AssetUtils::UpdateModelMatrix (gpu_loader.cpp:185-196). */
+int srt_update_model_matrix(srt_context* ctx, uint32_t index, const float frame[16]);
+/* light SSBO at binding 4 (src/main.cpp:688-692). */
+int srt_set_lights(srt_context* ctx, const srt_light* lights, uint32_t n);
+/* noiseTex / noiseUniformTex texel buffers at units 1,2 (src/main.cpp:269-301):
+ * RGB32F, `texels` = Width*Height each. */
+int srt_set_noise(srt_context* ctx, const float* noise_rgb, const float* noise_uniform_rgb, size_t texels);
+/* image0 (RGBA8 output) and image3 (RGBA32F accumulation), sized from the
+ * current Width/Height uniforms (and tiling).  Read back packed local rows. */
+int srt_alloc_images(srt_context* ctx);
+int srt_read_accum(srt_context* ctx, float* host_rgba32f, size_t bytes);
+int srt_read_output(srt_context* ctx, uint8_t* host_rgba8, size_t bytes);
+int srt_write_accum(srt_context* ctx, const float* host_rgba32f, size_t bytes);
+/* Device pointers of the images (for RCCL gathers without a host copy). */
+int srt_image_pointers(srt_context* ctx, void** accum_dev, void** out_dev);
+
+/* Closest-hit query: the test kernel ray_intersects.glsl:135-161 fed through
+ * AssetUtils::UpdateRays (gpu_loader.cpp:198-210); hits[i] = triangle index
+ * or 0xFFFFFFFF, t_out[i] = the final intersection_distance.  Host arrays. */
+int srt_trace_closest(srt_context* ctx, const srt_ray* rays, uint32_t n, uint32_t* hits, float* t_out);
+
+/* ===================== scene producers (host, CPU) ===================== */
+/* AssetUtils::LoadObject / ParseOBJ / ParseMTL / ConvertCPUGeometryToModel
+ * (src/asset_utils/model_loader.cpp:20-365) + BVH<GPU::Triangle>
+ * (include/intersection_utils/bvh.h:40-148).  `obj_path` is the .obj file;
+ * MTL files resolve relative to its directory. */
+int srt_model_load(const char* obj_path, srt_model** out);
+/* Build a model from raw triangles (one material). */
+int srt_model_from_triangles(const float* xyz9, uint32_t n_tris, const float kd[3], const float ks[3], float ns,
+                             srt_model** out);
+int srt_model_free(srt_model* m);
+/* counts: [0]=triangles [1]=vertices [2]=nodes [3]=leaves [4]=max depth [5]=materials [6]=faces dropped */
+int srt_model_info(const srt_model* m, uint64_t counts[8], float root_min[3], float root_max[3]);
+
+/* Flatten models exactly as UploadModelDataToGPU does (index rebasing). */
+int srt_scene_build(const srt_model* const* models, uint32_t n_models, srt_scene** out);
+int srt_scene_free(srt_scene* s);
+/* sizes: [0]=bvhs [1]=nodes [2]=materials [3]=triangles [4]=vertices */
+int srt_scene_sizes(const srt_scene* s, uint32_t sizes[5]);
+int srt_scene_copy(const srt_scene* s, srt_bvh_record* bvhs, srt_bvh_node* nodes, srt_material_obj* mats,
+                   float* tex_albedo, srt_triangle* tris, srt_vertex* verts);
+int srt_upload_scene_obj(srt_context* ctx, const srt_scene* s);
+
+/* Noise texel buffers of UpdateNoiseTex (src/main.cpp:269-301) from the
+ * never-seeded glibc rand() stream (include/common/utils.h:22-51).
+ * vec3 argument draw order: gcc_order != 0 draws z, y, x (g++, the
+ * reference's compiler); 0 draws x, y, z (clang).  Outputs RGB32F. */
+int srt_noise_generate(uint32_t texels, int gcc_order, float* noise_rgb, float* noise_uniform_rgb);
+/* glibc rand() (TYPE_3, seed 1) restated: first n outputs. */
+int srt_glibc_rand(uint32_t n, int32_t* out);
+
+/* Camera::Reset + UpdateCameraVectors (src/raytracer/camera.cpp:120-136,187-212):
+ * origin/front/up/right for the model (show_model != 0) or sphere scene. */
+int srt_camera_reset(int show_model, float origin[3], float front[3], float up[3], float right[3]);
+/* Camera::Rotate(yaw, pitch) basis from angles in degrees (camera.cpp:107-136). */
+int srt_camera_basis(float yaw_deg, float pitch_deg, float front[3], float up[3], float right[3]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

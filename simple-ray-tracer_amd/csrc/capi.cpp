@@ -1,0 +1,145 @@
+// capi.cpp -- C ABI of the host-side scene producers (include/srt_amd.h).
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "srt_internal.hpp"
+
+struct srt_model {
+  std::unique_ptr<srt::Model> m;
+};
+struct srt_scene {
+  std::unique_ptr<srt::Scene> s;
+};
+
+extern "C" {
+
+int srt_model_load(const char* obj_path, srt_model** out) {
+  if (!obj_path || !out) return SRT_ERR_INVALID;
+  std::string err;
+  auto m = srt::LoadObjectFile(obj_path, &err);
+  if (!m) {
+    srt::SetError(err);
+    return SRT_ERR_IO;
+  }
+  *out = new srt_model{std::move(m)};
+  return SRT_OK;
+}
+
+int srt_model_from_triangles(const float* xyz9, uint32_t n_tris, const float kd[3], const float ks[3], float ns,
+                             srt_model** out) {
+  if (!out || (n_tris && !xyz9) || !kd || !ks) return SRT_ERR_INVALID;
+  *out = new srt_model{srt::ModelFromTriangles(xyz9, n_tris, srt::Vec3(kd[0], kd[1], kd[2]),
+                                               srt::Vec3(ks[0], ks[1], ks[2]), ns)};
+  return SRT_OK;
+}
+
+int srt_model_free(srt_model* m) {
+  delete m;
+  return SRT_OK;
+}
+
+int srt_model_info(const srt_model* mm, uint64_t counts[8], float root_min[3], float root_max[3]) {
+  if (!mm || !mm->m || !counts) return SRT_ERR_INVALID;
+  const srt::Model& m = *mm->m;
+  counts[0] = m.prims.size();
+  counts[1] = m.vertices.size();
+  counts[2] = m.nodes.size();
+  counts[3] = m.leaves;
+  counts[4] = m.max_depth;
+  counts[5] = m.materials.size();
+  counts[6] = m.faces_dropped;
+  counts[7] = 0;
+  if (!m.nodes.empty()) {
+    if (root_min) {
+      root_min[0] = m.nodes[0].min_bounds.x; root_min[1] = m.nodes[0].min_bounds.y; root_min[2] = m.nodes[0].min_bounds.z;
+    }
+    if (root_max) {
+      root_max[0] = m.nodes[0].max_bounds.x; root_max[1] = m.nodes[0].max_bounds.y; root_max[2] = m.nodes[0].max_bounds.z;
+    }
+  }
+  return SRT_OK;
+}
+
+int srt_scene_build(const srt_model* const* models, uint32_t n_models, srt_scene** out) {
+  if (!out || (n_models && !models)) return SRT_ERR_INVALID;
+  std::vector<const srt::Model*> ms;
+  for (uint32_t i = 0; i < n_models; ++i) ms.push_back(models[i] ? models[i]->m.get() : nullptr);
+  std::string err;
+  auto s = srt::FlattenModels(ms, &err);
+  if (!s) {
+    srt::SetError(err);
+    return SRT_ERR_INVALID;
+  }
+  *out = new srt_scene{std::move(s)};
+  return SRT_OK;
+}
+
+int srt_scene_free(srt_scene* s) {
+  delete s;
+  return SRT_OK;
+}
+
+int srt_scene_sizes(const srt_scene* s, uint32_t sizes[5]) {
+  if (!s || !sizes) return SRT_ERR_INVALID;
+  sizes[0] = (uint32_t)s->s->bvhs.size();
+  sizes[1] = (uint32_t)s->s->nodes.size();
+  sizes[2] = (uint32_t)s->s->mats.size();
+  sizes[3] = (uint32_t)s->s->tris.size();
+  sizes[4] = (uint32_t)s->s->verts.size();
+  return SRT_OK;
+}
+
+int srt_scene_copy(const srt_scene* s, srt_bvh_record* bvhs, srt_bvh_node* nodes, srt_material_obj* mats,
+                   float* tex_albedo, srt_triangle* tris, srt_vertex* verts) {
+  if (!s) return SRT_ERR_INVALID;
+  const srt::Scene& sc = *s->s;
+  if (bvhs) std::memcpy(bvhs, sc.bvhs.data(), sc.bvhs.size() * sizeof(srt_bvh_record));
+  if (nodes) std::memcpy(nodes, sc.nodes.data(), sc.nodes.size() * sizeof(srt_bvh_node));
+  if (mats) std::memcpy(mats, sc.mats.data(), sc.mats.size() * sizeof(srt_material_obj));
+  if (tex_albedo) std::memcpy(tex_albedo, sc.tex_albedo.data(), sc.tex_albedo.size() * sizeof(float));
+  if (tris) std::memcpy(tris, sc.tris.data(), sc.tris.size() * sizeof(srt_triangle));
+  if (verts) std::memcpy(verts, sc.verts.data(), sc.verts.size() * sizeof(srt_vertex));
+  return SRT_OK;
+}
+
+int srt_upload_scene_obj(srt_context* ctx, const srt_scene* s) {
+  if (!ctx || !s) return SRT_ERR_INVALID;
+  const srt::Scene& sc = *s->s;
+  return srt_upload_scene(ctx, sc.bvhs.data(), (uint32_t)sc.bvhs.size(), sc.nodes.data(), (uint32_t)sc.nodes.size(),
+                          sc.mats.data(), sc.tex_albedo.data(), (uint32_t)sc.mats.size(), sc.tris.data(),
+                          (uint32_t)sc.tris.size(), sc.verts.data(), (uint32_t)sc.verts.size());
+}
+
+int srt_noise_generate(uint32_t texels, int gcc_order, float* noise_rgb, float* noise_uniform_rgb) {
+  if (!noise_rgb || !noise_uniform_rgb) return SRT_ERR_INVALID;
+  srt::GenerateNoise(texels, gcc_order != 0, noise_rgb, noise_uniform_rgb);
+  return SRT_OK;
+}
+
+int srt_glibc_rand(uint32_t n, int32_t* out) {
+  if (n && !out) return SRT_ERR_INVALID;
+  srt::GlibcRand(n, out);
+  return SRT_OK;
+}
+
+int srt_camera_reset(int show_model, float origin[3], float front[3], float up[3], float right[3]) {
+  srt::Vec3 o, f, u, r;
+  srt::CameraReset(show_model != 0, &o, &f, &u, &r);
+  if (origin) { origin[0] = o.x; origin[1] = o.y; origin[2] = o.z; }
+  if (front) { front[0] = f.x; front[1] = f.y; front[2] = f.z; }
+  if (up) { up[0] = u.x; up[1] = u.y; up[2] = u.z; }
+  if (right) { right[0] = r.x; right[1] = r.y; right[2] = r.z; }
+  return SRT_OK;
+}
+
+int srt_camera_basis(float yaw_deg, float pitch_deg, float front[3], float up[3], float right[3]) {
+  srt::Vec3 f, u, r;
+  srt::CameraBasis(yaw_deg, pitch_deg, &f, &u, &r);
+  if (front) { front[0] = f.x; front[1] = f.y; front[2] = f.z; }
+  if (up) { up[0] = u.x; up[1] = u.y; up[2] = u.z; }
+  if (right) { right[0] = r.x; right[1] = r.y; right[2] = r.z; }
+  return SRT_OK;
+}
+
+}  // extern "C"

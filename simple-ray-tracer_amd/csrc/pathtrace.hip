@@ -1,0 +1,1357 @@
+// pathtrace.hip -- MI355X (gfx950) path-tracing kernels + the device context.
+//
+// One HIP thread traces one pixel.  A launch covers `nframes` consecutive
+// frames of the reference's progressive loop (one dispatch of
+// shaders/raytrace_compute.glsl per frame, src/main.cpp:657-718); the
+// accumulation is carried in registers across frames (the same fp32 adds in
+// the same order as per-frame image RMWs) and stored once.
+//
+// Device layout (re-laid from the std430 SSBOs):
+//   nodes  : 32 B per node (min.xyz|first, max.xyz|count), base offset 32 B so
+//            each sibling pair (2k+1, 2k+2) is one 64-B aligned block;
+//   tris   : 48 B per triangle = v0, e1 = v1 - v0, e2 = v2 - v0, material id
+//            (vertex gather and edge subtraction hoisted to upload time);
+//   mats   : 32 B shading material (albedo|roughness, specular) precomputed
+//            from MaterialFromOBJ (raytrace_utils.glsl:140-175);
+//   lights : 32 B, one zero record appended (lights[lightCount] reads zero);
+//   noise  : noiseTex as .xy float2 (8 B), noiseUniformTex as .x float (4 B):
+//            the only channels the live kernel reads.
+// Traversal stack: per-lane in LDS (3 dwords per entry), sized from the
+// BVH's depth.  Shadow rays use an any-hit traversal, which returns exactly
+// CheckHit(...).hit (first accepted triangle happens before any change of the
+// running distance).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "pt_math.hpp"
+#include "srt_internal.hpp"
+
+using namespace srt::dev;
+
+namespace srt {
+
+// ---------------------------------------------------------------------------
+// kernel parameters (kernarg segment -> scalar registers)
+// ---------------------------------------------------------------------------
+struct KParams {
+  const float4* nodes;   // node i at nodes[2*i + 2], nodes[2*i + 3]
+  const float4* tris;    // 3 float4 per triangle
+  const float4* mats;    // 2 float4 per material
+  const float4* lights;  // 2 float4 per light, light_count + 1 records
+  const srt_bvh_record* bvhs;
+  const float2* noise_xy;
+  const float* noise_u;
+  float4* accum;
+  uint32_t* out;
+  unsigned long long* stats;
+  int W, H, WH;
+  int light_count;   // lightCount uniform (loop count)
+  int light_records; // records in the light SSBO; index >= light_records reads zeros
+  uint32_t bvh_count;
+  int show_model;
+  int max_depth;
+  int frame_first, nframes, write_output, reset;
+  int rank, nranks, band_rows, local_rows;
+  int ext_w, ext_h;
+  int stack_entries;
+  float cx, cy, cz, p00x, p00y, p00z, dux, duy, duz, dvx, dvy, dvz;
+};
+
+enum { ST_RAYS = 0, ST_NODES, ST_TRIS, ST_RNGU, ST_RNGSQ, ST_LIGHTS, ST_MATS, ST_SAMPLES, ST_OVERFLOW, ST_MAXSTACK, ST_N };
+
+struct Counters {
+  uint32_t v[ST_N];
+};
+
+template <bool COUNT>
+__device__ __forceinline__ void bump(Counters& c, int k, uint32_t n = 1) {
+  if constexpr (COUNT) c.v[k] += n;
+}
+
+struct Mat {
+  f3 albedo, specular;
+  float roughness, metalness;
+  bool useSpec;
+};
+
+struct Hit {
+  bool hit;
+  f3 p, normal;
+  Mat mat;
+};
+
+struct LightRec {
+  f3 pos;
+  float intensity;
+  f3 color;
+};
+
+// raytrace_compute.glsl:299-364: five hard-coded spheres and their materials
+__device__ __forceinline__ void sphere_data(int i, f3& pos, float& radius, Mat& m) {
+  switch (i) {
+    case 0: pos = mk(1.8f, 0.0f, -2.0f); radius = 0.5f;   // blue (material4)
+      m = Mat{mk(0.2f, 0.4f, 1.0f), mk(0.8f, 0.8f, 0.9f), 0.01f, 0.9f, false}; break;
+    case 1: pos = mk(0.0f, -100.5f, -1.0f); radius = 100.0f;  // ground (material1)
+      m = Mat{mk(0.2f, 0.8f, 0.8f), mk(0.2f, 0.4f, 0.4f), 0.01f, 0.99f, false}; break;
+    case 2: pos = mk(0.55f, 0.0f, -2.0f); radius = 0.5f;  // green (material3)
+      m = Mat{mk(0.2f, 0.9f, 0.3f), mk(0.2f, 0.9f, 0.9f), 0.3f, 0.95f, true}; break;
+    case 3: pos = mk(-0.55f, 0.0f, -2.0f); radius = 0.5f;  // red (material2)
+      m = Mat{mk(0.8f, 0.3f, 0.3f), mk(0.9f, 0.7f, 0.7f), 0.1f, 0.5f, true}; break;
+    default: pos = mk(-1.8f, 0.0f, -2.0f); radius = 0.5f;  // yellow (material5)
+      m = Mat{mk(0.9f, 0.8f, 0.1f), mk(0.3f, 0.3f, 0.1f), 0.7f, 0.3f, false}; break;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// per-lane context
+// ---------------------------------------------------------------------------
+struct Lane {
+  int base;             // (y * Height) + x  (raytrace_utils.glsl:11-12,45-46)
+  uint32_t* stk;        // LDS stack: entry k field f at stk[(3k+f) * stride]
+  int stride;
+};
+
+// raytrace_utils.glsl:28-30
+__device__ __forceinline__ float rand_float(float sx, float sy) {
+  const float d = sx * 12.9898f + sy * 78.233f;
+  return fractf(sin_f(d) * 43758.5453f);
+}
+
+// raytrace_utils.glsl:44-54 randFloatSampleUniform
+template <bool COUNT>
+__device__ __forceinline__ float randU(const KParams& kp, const Lane& ln, Counters& c, float sx, float sy) {
+  const float r = rand_float(sx, sy) * (float)kp.W * (float)kp.H;
+  const int idx = (ln.base + f2i(r)) % kp.WH;
+  bump<COUNT>(c, ST_RNGU);
+  return kp.noise_u[idx];
+}
+
+__device__ __forceinline__ float luminance(f3 c) { return c.x * 0.2126f + c.y * 0.7152f + c.z * 0.0722f; }
+__device__ __forceinline__ f3 specularF0(f3 b, float m) {
+  const float om = 1.0f - m;
+  return mk(0.04f * om + b.x * m, 0.04f * om + b.y * m, 0.04f * om + b.z * m);
+}
+__device__ __forceinline__ f3 perpendicular(f3 u) {
+  const f3 a = mk(__builtin_fabsf(u.x), __builtin_fabsf(u.y), __builtin_fabsf(u.z));
+  const unsigned xm = ((a.x - a.y) < 0.0f && (a.x - a.z) < 0.0f) ? 1u : 0u;
+  const unsigned ym = (a.y - a.z) < 0.0f ? (1u ^ xm) : 0u;
+  const unsigned zm = 1u ^ (xm | ym);
+  return cross(u, mk((float)xm, (float)ym, (float)zm));
+}
+__device__ __forceinline__ float shadowedF90(f3 F0) { return fmn(1.0f, (1.0f / 0.04f) * luminance(F0)); }
+__device__ __forceinline__ f3 fresnelSchlickNew(f3 f0, float f90, float NdotS) {
+  const float p = pow_f(1.0f - NdotS, 5.0f);
+  return f0 + mk(f90 - f0.x, f90 - f0.y, f90 - f0.z) * p;
+}
+__device__ __forceinline__ f3 schlickFresnel(f3 f0, float u) {
+  const float p = pow_f(fmx(0.001f, 1.0f - u), 5.0f);
+  return f0 + (mk(1.0f, 1.0f, 1.0f) - f0) * p;
+}
+__device__ __forceinline__ float linearToSrgb(float c) {
+  if (c < 0.0031308f) return c * 12.92f;
+  return 1.055f * pow_f(c, 1.0f / 2.4f) - 0.055f;
+}
+__device__ __forceinline__ uint32_t to_unorm8(float x) {
+  if (x != x) return 0u;
+  return (uint32_t)__builtin_rintf(clampf(x, 0.0f, 1.0f) * 255.0f);
+}
+
+// ---------------------------------------------------------------------------
+// BVH traversal (ray_intersects.glsl:49-133), order-exact
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float box_t(f3 o, f3 inv, float4 lo, float4 hi) {
+  const float t0x = (lo.x - o.x) * inv.x, t0y = (lo.y - o.y) * inv.y, t0z = (lo.z - o.z) * inv.z;
+  const float t1x = (hi.x - o.x) * inv.x, t1y = (hi.y - o.y) * inv.y, t1z = (hi.z - o.z) * inv.z;
+  const float tn = fmx(fmx(fmn(t0x, t1x), fmn(t0y, t1y)), fmn(t0z, t1z));
+  const float tf = fmn(fmn(fmx(t0x, t1x), fmx(t0y, t1y)), fmx(t0z, t1z));
+  return tn <= tf ? ((tn >= 0.0f) ? tn : tf) : __builtin_inff();
+}
+
+__device__ __forceinline__ bool box_ok(float b, float dist) { return b < dist && !isinf_f(b); }
+
+// Moller-Trumbore with precomputed edges (ray_intersects.glsl:61-96)
+__device__ __forceinline__ bool tri_test(f3 o, f3 d, const float4* tp, float& dist) {
+  const float4 A = tp[0], B = tp[1], C = tp[2];
+  const f3 v0 = mk(A.x, A.y, A.z), e1 = mk(A.w, B.x, B.y), e2 = mk(B.z, B.w, C.x);
+  const f3 h = cross(d, e2);
+  const float a = dot(e1, h);
+  if (a > -0.0001f && a < 0.0001f) return false;
+  const float f = 1.0f / a;
+  const f3 s = o - v0;
+  const float u = f * dot(s, h);
+  if (u < 0.0f || u > 1.0f) return false;
+  const f3 q = cross(s, e1);
+  const float v = f * dot(d, q);
+  if (v < 0.0f || u + v > 1.0f) return false;
+  const float t = f * dot(e2, q);
+  if (t > 0.00001f && t < dist) {
+    dist = t;
+    return true;
+  }
+  return false;
+}
+
+// Depth-first traversal in the reference's pop order (right child first).
+// Each child's box is tested once, when its parent is expanded; a child that
+// fails is never pushed (the running distance only shrinks, so it would fail
+// at its pop too); a pushed child is re-checked against the distance at pop
+// time with its stored entry distance (the same value IntersectsBox returns).
+template <bool ANY, bool COUNT>
+__device__ uint32_t traverse(const KParams& kp, const Lane& ln, Counters& c, uint32_t root, f3 o, f3 d,
+                             float& dist) {
+  const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  uint32_t hit = 0xFFFFFFFFu;
+  const float4* N = kp.nodes;
+  float4 lo = N[2 * root + 2], hi = N[2 * root + 3];
+  bump<COUNT>(c, ST_NODES);
+  if (!box_ok(box_t(o, inv, lo, hi), dist)) return hit;
+  uint32_t ref = __float_as_uint(lo.w), cnt = __float_as_uint(hi.w);
+  int sp = 0;
+  for (;;) {
+    if (cnt > 0) {
+      for (uint32_t i = 0; i < cnt; ++i) {
+        bump<COUNT>(c, ST_TRIS);
+        if (tri_test(o, d, kp.tris + 3 * (size_t)(ref + i), dist)) {
+          hit = ref + i;
+          if constexpr (ANY) return hit;
+        }
+      }
+    } else {
+      const float4* P = N + 2 * (size_t)ref + 2;
+      const float4 l0 = P[0], h0 = P[1], l1 = P[2], h1 = P[3];
+      bump<COUNT>(c, ST_NODES, 2);
+      const float b0 = box_t(o, inv, l0, h0);
+      const float b1 = box_t(o, inv, l1, h1);
+      const bool v0 = box_ok(b0, dist), v1 = box_ok(b1, dist);
+      if (v0) {
+        if (sp >= kp.stack_entries) {  // cannot happen for a validated BVH
+          bump<COUNT>(c, ST_OVERFLOW);
+          return hit;
+        }
+        ln.stk[(3 * sp + 0) * ln.stride] = __float_as_uint(l0.w);
+        ln.stk[(3 * sp + 1) * ln.stride] = __float_as_uint(h0.w);
+        ln.stk[(3 * sp + 2) * ln.stride] = __float_as_uint(b0);
+        ++sp;
+        if constexpr (COUNT) {
+          if ((uint32_t)sp + 1 > c.v[ST_MAXSTACK]) c.v[ST_MAXSTACK] = (uint32_t)sp + 1;
+        }
+      }
+      if (v1) {
+        ref = __float_as_uint(l1.w);
+        cnt = __float_as_uint(h1.w);
+        continue;
+      }
+    }
+    // pop the next entry that still beats the running distance
+    bool found = false;
+    while (sp > 0) {
+      --sp;
+      const float bt = __uint_as_float(ln.stk[(3 * sp + 2) * ln.stride]);
+      if (bt < dist) {
+        ref = ln.stk[(3 * sp + 0) * ln.stride];
+        cnt = ln.stk[(3 * sp + 1) * ln.stride];
+        found = true;
+        break;
+      }
+    }
+    if (!found) break;
+  }
+  return hit;
+}
+
+// raytrace_compute.glsl:93-120 SphereHit
+__device__ __forceinline__ bool sphere_hit(f3 ro, f3 rd, f3 pos, float radius, float mn, float mx, float& t) {
+  const f3 oc = pos - ro;
+  const float ld = length(rd);
+  const float a = ld * ld;
+  const float h = dot(rd, oc);
+  const float loc = length(oc);
+  const float cc = loc * loc - (radius * radius);
+  const float disc = h * h - a * cc;
+  if (disc < 0.0f) return false;
+  const float sq = __builtin_sqrtf(disc);
+  float root = (h - sq) / a;
+  if (!(mn < root && root < mx)) {
+    root = (h + sq) / a;
+    if (!(mn < root && root < mx)) return false;
+  }
+  t = root;
+  return true;
+}
+
+__device__ __forceinline__ f3 xform(const float* m, f3 v, float w) {
+  return mk(((m[0] * v.x + m[4] * v.y) + m[8] * v.z) + m[12] * w,
+            ((m[1] * v.x + m[5] * v.y) + m[9] * v.z) + m[13] * w,
+            ((m[2] * v.x + m[6] * v.y) + m[10] * v.z) + m[14] * w);
+}
+
+// raytrace_compute.glsl:122-165 CheckHit (closest hit, full record)
+template <bool COUNT>
+__device__ Hit check_hit(const KParams& kp, const Lane& ln, Counters& c, f3 ro, f3 rd, float mn, float mx) {
+  Hit rec;
+  rec.hit = false;
+  bump<COUNT>(c, ST_RAYS);
+  float dist = mx;
+  if (!kp.show_model) {
+    int best = -1;
+    f3 best_p = mk(0.f, 0.f, 0.f);
+    float best_t = 0.f;
+    for (int i = 0; i < 5; ++i) {
+      f3 pos; float radius; Mat m;
+      sphere_data(i, pos, radius, m);
+      float t;
+      if (sphere_hit(ro, rd, pos, radius, mn, dist, t)) {
+        best = i;
+        best_t = t;
+        dist = t;
+      }
+    }
+    if (best >= 0) {
+      f3 pos; float radius; Mat m;
+      sphere_data(best, pos, radius, m);
+      rec.hit = true;
+      best_p = ro + rd * best_t;
+      rec.p = best_p;
+      rec.mat = m;
+      const f3 outward = (best_p - pos) / radius;   // SetFaceNormal (raytrace_utils.glsl:23-26)
+      rec.normal = (dot(rd, outward) < 0.0f) ? outward : -outward;
+    }
+  } else {
+    uint32_t hit_tri = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < kp.bvh_count; ++i) {
+      const srt_bvh_record& b = kp.bvhs[i];
+      const f3 to = xform(b.frame, ro, 1.0f);
+      const f3 td = xform(b.frame, rd, 0.0f);
+      const uint32_t h = traverse<false, COUNT>(kp, ln, c, b.first_index, to, td, dist);
+      if (h != 0xFFFFFFFFu) hit_tri = h;
+    }
+    if (hit_tri != 0xFFFFFFFFu) {
+      rec.hit = true;
+      rec.p = (dist * rd) + ro;
+      const float4* tp = kp.tris + 3 * (size_t)hit_tri;
+      const float4 A = tp[0], B = tp[1], C = tp[2];
+      const f3 e1 = mk(A.w, B.x, B.y), e2 = mk(B.z, B.w, C.x);
+      rec.normal = normalize(cross(e1, e2));
+      const uint32_t mi = __float_as_uint(C.y);
+      const float4 m0 = kp.mats[2 * mi], m1 = kp.mats[2 * mi + 1];
+      bump<COUNT>(c, ST_MATS);
+      rec.mat.albedo = mk(m0.x, m0.y, m0.z);
+      rec.mat.roughness = m0.w;
+      rec.mat.specular = mk(m1.x, m1.y, m1.z);
+      rec.mat.metalness = 0.1f;
+      rec.mat.useSpec = true;
+    }
+  }
+  return rec;
+}
+
+// CheckHit(...).hit for the shadow ray of CheckLightOccluded (raytrace_compute.glsl:167-176)
+template <bool COUNT>
+__device__ bool any_hit(const KParams& kp, const Lane& ln, Counters& c, f3 ro, f3 rd, float mn, float mx) {
+  bump<COUNT>(c, ST_RAYS);
+  if (!kp.show_model) {
+    for (int i = 0; i < 5; ++i) {
+      f3 pos; float radius; Mat m;
+      sphere_data(i, pos, radius, m);
+      float t;
+      if (sphere_hit(ro, rd, pos, radius, mn, mx, t)) return true;
+    }
+    return false;
+  }
+  for (uint32_t i = 0; i < kp.bvh_count; ++i) {
+    const srt_bvh_record& b = kp.bvhs[i];
+    const f3 to = xform(b.frame, ro, 1.0f);
+    const f3 td = xform(b.frame, rd, 0.0f);
+    float dist = mx;
+    if (traverse<true, COUNT>(kp, ln, c, b.first_index, to, td, dist) != 0xFFFFFFFFu) return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ float light_falloff(f3 p, const LightRec& L) {
+  const f3 d = L.pos - p;
+  const float d2 = dot(d, d);
+  return 1.0f / ((0.01f * 0.01f) + d2);
+}
+__device__ __forceinline__ f3 light_dir(const LightRec& L, f3 p) {
+  const f3 ld = L.pos - p;
+  return length(ld) > 0.0f ? normalize(ld) : ld;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ LightRec load_light(const KParams& kp, Counters& c, int idx) {
+  bump<COUNT>(c, ST_LIGHTS);
+  const int i = (idx >= 0 && idx < kp.light_records) ? idx : kp.light_records;  // zero record
+  const float4 a = kp.lights[2 * i], b = kp.lights[2 * i + 1];
+  return LightRec{mk(a.x, a.y, a.z), a.w, mk(b.x, b.y, b.z)};
+}
+
+// raytrace_compute.glsl:179-206 SampleLights.  randLightIndex uses the same
+// seed every iteration, so the light (and its pdf) is loop-invariant; once a
+// light is selected later iterations only re-select it, so their random
+// draws are skipped (the result is unchanged).
+template <bool COUNT>
+__device__ bool sample_lights(const KParams& kp, const Lane& ln, Counters& c, f3 p, float& weight, LightRec& sel) {
+  const int n = kp.light_count;
+  float total = 0.0f, pdf = 0.0f;
+  bool selected = false;
+  if (n > 0) {
+    const int idx = f2i(__builtin_rintf(randU<COUNT>(kp, ln, c, p.x, p.y) * (float)n));
+    sel = load_light<COUNT>(kp, c, idx);
+    const float fo = light_falloff(p, sel);
+    const float inten = sel.intensity * fo;
+    const float lpdf = luminance(mk(inten, inten, inten));
+    const float ris = lpdf * (float)n;
+    for (int i = 0; i < n; ++i) {
+      total += ris;
+      if (!selected) {
+        const float r = randU<COUNT>(kp, ln, c, p.y + (float)i, p.z + (float)i);
+        if (r < (ris / total)) {
+          pdf = lpdf;
+          selected = true;
+        }
+      }
+    }
+  }
+  weight = (total / (float)n) / fmx(0.001f, pdf);
+  return selected;
+}
+
+__device__ __forceinline__ float ggxD(float NdotH, float rough) {
+  const float a2 = rough * rough;
+  const float d = ((NdotH * a2 - NdotH) * NdotH + 1.0f);
+  return a2 / fmx(0.001f, (d * d * 3.1415926535897f));
+}
+__device__ __forceinline__ float ggxDNew(float NdotH, float alphaSquared) {
+  const float b = ((alphaSquared - 1.0f) * NdotH * NdotH + 1.0f);
+  return alphaSquared / fmx(0.001f, (3.1415926535897f * b * b));
+}
+__device__ __forceinline__ float ggxSchlickMasking(float NdotL, float NdotV, float rough) {
+  const float k = rough * rough / 2.0f;
+  const float gv = NdotV / fmx(0.001f, (NdotV * (1.0f - k) + k));
+  const float gl = NdotL / fmx(0.001f, (NdotL * (1.0f - k) + k));
+  return __builtin_fabsf(gv * gl);
+}
+__device__ __forceinline__ float smithGAlpha(float alpha, float NdotS) {
+  return NdotS / (fmx(0.0001f, alpha) * __builtin_sqrtf(1.0f - fmn(0.99999f, NdotS * NdotS)));
+}
+__device__ __forceinline__ float smithLambda(float a) {
+  return (-1.0f + __builtin_sqrtf(1.0f + (1.0f / fmx(0.001f, a * a)))) * 0.5f;
+}
+__device__ __forceinline__ float smithG2(float alpha, float NdotL, float NdotV) {
+  const float aL = smithGAlpha(alpha, NdotL);
+  const float aV = smithGAlpha(alpha, NdotV);
+  return 1.0f / (1.0f + smithLambda(aL) + smithLambda(aV));
+}
+
+// brdf.glsl:200-224 SampleDirect
+__device__ f3 sample_direct(const Hit& hit, f3 Vv, const LightRec& L, float shadow) {
+  const f3 Ld = light_dir(L, hit.p);
+  const f3 vl = Vv + Ld;
+  const f3 H = length(vl) > 0.0f ? normalize(vl) : vl;
+  const f3 N = hit.normal;
+  const float NdotL = sat(dot(N, Ld));
+  const float NdotH = sat(dot(N, H));
+  const float LdotH = sat(dot(Ld, H));
+  const float NdotV = sat(dot(N, Vv));
+  const float rough = hit.mat.roughness;
+  const float D = ggxD(NdotH, rough);
+  const float G = ggxSchlickMasking(NdotL, NdotV, rough);
+  const f3 F = schlickFresnel(hit.mat.specular, LdotH);
+  const float fo = light_falloff(hit.p, L);
+  const float li = L.intensity * fo;
+  const f3 ggx = (F * (D * G)) / (4.0f * fmx(0.001f, NdotV));
+  const f3 lt = (shadow * L.color) * li;
+  const f3 diff = (NdotL * hit.mat.albedo) / 3.1415926535897f;
+  return lt * (ggx + diff);
+}
+
+// brdf.glsl:226-237 SampleDirectNew (GetAllBRDFValues :173-198, EvalSpecular :139-145
+// with ggxNormalDistributionNew's arguments swapped as in the reference, EvalDiffuse :134-137)
+__device__ f3 sample_direct_new(const Hit& hit, f3 Vv, f3 L) {
+  const f3 N = hit.normal;
+  const f3 H = normalize(L + Vv);
+  const float NdotL = sat(dot(N, L));
+  const float NdotV = sat(dot(N, Vv));
+  const float LdotH = sat(dot(L, H));
+  const float NdotH = sat(dot(N, H));
+  const f3 specF0 = specularF0(hit.mat.albedo, hit.mat.metalness);
+  const f3 diffRefl = hit.mat.albedo * (1.0f - hit.mat.metalness);
+  const float alpha = hit.mat.roughness * hit.mat.roughness;
+  const float alphaSq = alpha * alpha;
+  const f3 F = fresnelSchlickNew(specF0, shadowedF90(specF0), LdotH);
+  const float D = ggxDNew(fmx(0.00001f, alphaSq), NdotH);
+  const float G = smithG2(alpha, NdotL, NdotV);
+  const float denom = 4.0f * fmx(NdotL, 0.001f) * fmx(NdotV, 0.001f);
+  const f3 spec = (((F * G) * D) / fmx(denom, 0.001f)) * NdotL;
+  const float oneOverPi = 1.0f / 3.1415926535897f;
+  const f3 diff = diffRefl * (oneOverPi * NdotL);
+  return ((mk(1.0f, 1.0f, 1.0f) - F) * diff) + spec;
+}
+
+// brdf.glsl:279-288
+__device__ float brdf_probability(const Mat& m, f3 Vv, f3 N) {
+  const float sF0 = luminance(specularF0(m.albedo, m.metalness));
+  const float dR = luminance(m.albedo * (1.0f - m.metalness));
+  const f3 f0 = mk(sF0, sF0, sF0);
+  const float F = sat(luminance(fresnelSchlickNew(f0, shadowedF90(f0), fmx(0.0f, dot(Vv, N)))));
+  const float diffuse = dR * (1.0f - F);
+  const float p = (F / fmx(0.0001f, (F + diffuse)));
+  return clampf(p, 0.1f, 0.9f);
+}
+
+// brdf.glsl:81-99 SampleSpecularHalfVec given its two uniform draws
+__device__ __forceinline__ f3 specular_half(float rx, float ry, float rough, f3 N) {
+  const f3 B = perpendicular(N);
+  const f3 T = cross(B, N);
+  const float a2 = rough * rough;
+  const float cosT = __builtin_sqrtf(fmx(0.0f, (1.0f - rx) / ((a2 - 1.0f) * rx + 1.0f)));
+  const float sinT = __builtin_sqrtf(fmx(0.0f, 1.0f - cosT * cosT));
+  const float phi = ry * 3.1415926535897f * 2.0f;
+  return ((T * (sinT * cos_f(phi))) + (B * (sinT * sin_f(phi)))) + (N * cosT);
+}
+
+__device__ __forceinline__ f3 reflect3(f3 I, f3 N) { return I - N * (2.0f * dot(N, I)); }
+
+#define DIFFUSE_BRDF 1
+#define SPECULAR_BRDF 2
+
+// brdf.glsl:239-277 SampleIndirectNew.  SampleDiffuse (:60-74) and
+// SampleSpecularHalfVec (:81-99) draw the same two numbers (seeds p.xy, p.yz).
+template <bool COUNT>
+__device__ bool sample_indirect(const KParams& kp, const Lane& ln, Counters& c, const Hit& hit, f3 Vv, int type,
+                                f3& dir, f3& weight) {
+  const f3 N = hit.normal;
+  if (dot(N, Vv) <= 0.0f) return false;
+  const f3 specF0 = specularF0(hit.mat.albedo, hit.mat.metalness);
+  f3 nd;
+  if (type == DIFFUSE_BRDF) {
+    const float r1 = randU<COUNT>(kp, ln, c, hit.p.x, hit.p.y);
+    const float r2 = randU<COUNT>(kp, ln, c, hit.p.y, hit.p.z);
+    const f3 B = perpendicular(N);
+    const f3 T = cross(B, N);
+    const float r = __builtin_sqrtf(__builtin_fabsf(r1));
+    const float phi = 2.0f * 3.1415926535897f * r2;
+    nd = ((T * (r * cos_f(phi))) + (B * (r * sin_f(phi)))) + (N * __builtin_sqrtf(__builtin_fabsf(1.0f - r1)));
+    weight = hit.mat.albedo * (1.0f - hit.mat.metalness);
+    const f3 H = specular_half(r1, r2, hit.mat.roughness, N);
+    const float VdotH = fmx(0.00001f, fmn(1.0f, dot(Vv, H)));
+    weight = weight * (mk(1.0f, 1.0f, 1.0f) - fresnelSchlickNew(specF0, shadowedF90(specF0), VdotH));
+  } else {
+    // brdf.glsl:102-132 SampleSpecularMicrofacet
+    const float alpha = hit.mat.roughness * hit.mat.roughness;
+    const float alphaSq = alpha * alpha;
+    f3 H;
+    if (alpha == 0.0f) {
+      const f3 Lt = reflect3(-Vv, N);
+      H = normalize(-Vv + Lt);
+    } else {
+      const float rx = randU<COUNT>(kp, ln, c, hit.p.x, hit.p.y);
+      const float ry = randU<COUNT>(kp, ln, c, hit.p.y, hit.p.z);
+      H = specular_half(rx, ry, hit.mat.roughness, N);
+    }
+    const f3 L = reflect3(-Vv, H);
+    const float HdotL = fmx(0.00001f, fmn(1.0f, dot(H, L)));
+    const float NdotL = fmx(0.00001f, fmn(1.0f, dot(N, L)));
+    const f3 F = fresnelSchlickNew(specF0, shadowedF90(specF0), HdotL);
+    const float N2 = NdotL * NdotL;
+    weight = F * (2.0f / (__builtin_sqrtf(((alphaSq * (1.0f - N2)) + N2) / N2) + 1.0f));
+    nd = L;
+  }
+  if (luminance(weight) == 0.0f) return false;
+  dir = normalize(nd);
+  if (dot(N, dir) <= 0.0f) return false;
+  return true;
+}
+
+// raytrace_compute.glsl:208-294 GetRayColor
+template <bool COUNT>
+__device__ f3 ray_color(const KParams& kp, const Lane& ln, Counters& c, f3 ro, f3 rd) {
+  int randIndex = 0;
+  int depth = kp.max_depth;
+  f3 T = mk(1.0f, 1.0f, 1.0f);
+  f3 color = mk(0.0f, 0.0f, 0.0f);
+  for (;;) {
+    const Hit rec = check_hit<COUNT>(kp, ln, c, ro, rd, 0.001f, __builtin_inff());
+    if (!rec.hit) break;
+    float lw;
+    LightRec L;
+    const bool sampled = sample_lights<COUNT>(kp, ln, c, rec.p, lw, L);
+    const f3 Vv = -rd;
+    if (sampled) {
+      const f3 toL = L.pos - rec.p;
+      const f3 sdir = normalize(toL);
+      const float smax = length(toL);
+      const float shadow = any_hit<COUNT>(kp, ln, c, rec.p, sdir, 0.001f, smax) ? 0.0f : 1.0f;
+      if (rec.mat.useSpec) {
+        color = color + (T * sample_direct(rec, Vv, L, shadow)) * lw;
+      } else {
+        const f3 Ld = light_dir(L, rec.p);
+        const float fo = light_falloff(rec.p, L);
+        const f3 li = ((L.color * fo) * L.intensity) * lw;
+        color = color + ((T * sample_direct_new(rec, Vv, Ld)) * shadow) * li;
+      }
+    }
+    int type;
+    if (rec.mat.metalness == 1.0f && rec.mat.roughness == 0.0f) {
+      type = SPECULAR_BRDF;
+    } else {
+      const float bp = brdf_probability(rec.mat, Vv, rec.normal);
+      const float r = randU<COUNT>(kp, ln, c, rec.p.x + (float)depth, rec.p.y + (float)depth);
+      if (r < bp) {
+        type = SPECULAR_BRDF;
+        T = T / bp;
+      } else {
+        type = DIFFUSE_BRDF;
+        T = T / (1.0f - bp);
+      }
+    }
+    if (depth <= 0) {
+      const float surv = clampf(luminance(T), 0.1f, 1.0f);
+      if (randU<COUNT>(kp, ln, c, rec.p.x + (float)randIndex, rec.p.y + (float)randIndex) > surv) break;
+      T = T / surv;
+      randIndex++;
+    } else {
+      depth--;
+    }
+    f3 dir, bw;
+    if (!sample_indirect<COUNT>(kp, ln, c, rec, Vv, type, dir, bw)) break;
+    T = T * bw;
+    rd = dir;
+    ro = rec.p;
+  }
+  return color + T * mk(0.05f, 0.05f, 0.05f);
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void flush_counters(const KParams& kp, const Counters& c) {
+  if constexpr (COUNT) {
+    for (int k = 0; k < ST_N; ++k) {
+      if (k == ST_MAXSTACK) {
+        atomicMax(&kp.stats[k], (unsigned long long)c.v[k]);
+      } else if (c.v[k]) {
+        atomicAdd(&kp.stats[k], (unsigned long long)c.v[k]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+// Pixel mapping: a 256-thread block covers 16x16 local pixels as four 8x8
+// wave tiles (the reference's local_size 8x8, raytrace_compute.glsl:12).
+template <bool COUNT>
+__global__ __launch_bounds__(256) void pathtrace_kernel(KParams kp) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+  const int ly = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+  if (x >= kp.ext_w || ly >= kp.local_rows) return;
+  const int band = ly / kp.band_rows;
+  const int gy = (band * kp.nranks + kp.rank) * kp.band_rows + (ly - band * kp.band_rows);
+  if (gy >= kp.ext_h) return;
+  const size_t li = (size_t)ly * (size_t)kp.W + (size_t)x;
+  if (kp.reset) {  // raytrace_compute.glsl:390-393
+    kp.accum[li] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+    return;
+  }
+  Lane ln;
+  ln.base = gy * kp.H + x;
+  ln.stk = lds + tid;
+  ln.stride = blockDim.x;
+  Counters c;
+  for (int k = 0; k < ST_N; ++k) c.v[k] = 0;
+  const f3 center = mk(kp.cx, kp.cy, kp.cz);
+  const f3 p00 = mk(kp.p00x, kp.p00y, kp.p00z);
+  const f3 du = mk(kp.dux, kp.duy, kp.duz);
+  const f3 dv = mk(kp.dvx, kp.dvy, kp.dvz);
+  const float4 a0 = kp.accum[li];
+  f3 acc = mk(a0.x, a0.y, a0.z);
+  for (int k = 0; k < kp.nframes; ++k) {
+    const int frame = kp.frame_first + k;
+    const int samp = frame % kp.WH;                              // raytrace_compute.glsl:400
+    const float2 nz = kp.noise_xy[(ln.base + samp) % kp.WH];     // SampleSquare, raytrace_utils.glsl:10-17
+    bump<COUNT>(c, ST_RNGSQ);
+    bump<COUNT>(c, ST_SAMPLES);
+    const float ox = nz.x - 0.5f, oy = nz.y - 0.5f;
+    const f3 ps = (p00 + du * ((float)x + ox)) + dv * ((float)gy + oy);   // GetRay :78-90
+    const f3 rd = ps - center;
+    acc = acc + ray_color<COUNT>(kp, ln, c, center, rd);
+  }
+  kp.accum[li] = make_float4(acc.x, acc.y, acc.z, 1.0f);
+  if (kp.write_output) {  // raytrace_compute.glsl:412-413
+    const f3 o = acc / (float)(kp.frame_first + kp.nframes - 1);
+    const uint32_t r = to_unorm8(linearToSrgb(o.x)), g = to_unorm8(linearToSrgb(o.y)),
+                   b = to_unorm8(linearToSrgb(o.z));
+    kp.out[li] = r | (g << 8) | (b << 16) | (255u << 24);
+  }
+  flush_counters<COUNT>(kp, c);
+}
+
+// The closest-hit test kernel of ray_intersects.glsl:135-161.
+__global__ __launch_bounds__(256) void closest_kernel(KParams kp, const srt_ray* rays, uint32_t n, uint32_t* hits,
+                                                      float* tout) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Lane ln;
+  ln.base = 0;
+  ln.stk = lds + threadIdx.x;
+  ln.stride = blockDim.x;
+  Counters c;
+  for (int k = 0; k < ST_N; ++k) c.v[k] = 0;
+  const srt_ray r = rays[i];
+  const f3 o = mk(r.origin[0], r.origin[1], r.origin[2]);
+  const f3 d = mk(r.direction[0], r.direction[1], r.direction[2]);
+  float dist = r.intersection_distance;
+  uint32_t hit = 0xFFFFFFFFu;
+  for (uint32_t b = 0; b < kp.bvh_count; ++b) {
+    const srt_bvh_record& rec = kp.bvhs[b];
+    const uint32_t h = traverse<false, true>(kp, ln, c, rec.first_index, xform(rec.frame, o, 1.0f),
+                                             xform(rec.frame, d, 0.0f), dist);
+    if (h != 0xFFFFFFFFu) hit = h;
+  }
+  hits[i] = hit;
+  tout[i] = dist;
+  flush_counters<true>(kp, c);
+}
+
+}  // namespace srt
+
+// ===========================================================================
+// host side: the device context behind the C ABI
+// ===========================================================================
+namespace srt {
+
+static std::mutex g_err_mu;
+static std::string g_err;
+void SetError(const std::string& msg) {
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  g_err = msg;
+}
+const char* LastError() {
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  return g_err.c_str();
+}
+
+}  // namespace srt
+
+#define HIP_OK(expr)                                                                          \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess) {                                                                   \
+      srt::SetError(std::string(#expr) + ": " + hipGetErrorString(e_));                     \
+      return SRT_ERR_HIP;                                                                     \
+    }                                                                                         \
+  } while (0)
+
+struct srt_context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  // uniforms
+  int W = 0, H = 0, accum_frames = 0, reset = 0, show_model = 0, light_count = 0, max_depth = 5;
+  uint32_t bvh_count = 0;
+  float cam_origin[3] = {0, 0, 0}, cam_dir[3] = {0, 0, -1}, cam_up[3] = {0, 1, 0}, cam_right[3] = {1, 0, 0};
+  // tiling
+  int rank = 0, nranks = 1, band_rows = 16;
+  // scene
+  float4* d_nodes = nullptr;
+  float4* d_tris = nullptr;
+  float4* d_mats = nullptr;
+  srt_bvh_record* d_bvhs = nullptr;
+  uint32_t bvh_capacity = 0;
+  std::vector<srt_bvh_record> h_bvhs;
+  uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
+  int stack_entries = 1;
+  bool scene_ok = false;
+  // lights
+  std::vector<srt_light> h_lights;
+  float4* d_lights = nullptr;
+  uint32_t light_capacity = 0;
+  bool lights_dirty = true;
+  // noise
+  float2* d_noise_xy = nullptr;
+  float* d_noise_u = nullptr;
+  size_t noise_texels = 0;
+  // images
+  float4* d_accum = nullptr;
+  uint32_t* d_out = nullptr;
+  int img_w = 0, img_rows = 0;
+  // stats
+  unsigned long long* d_stats = nullptr;
+  srt_stats stats{};
+};
+
+namespace {
+
+void FreeDev(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+int LocalRows(const srt_context* c, int H) {
+  int rows = 0;
+  const int nb = (H + c->band_rows - 1) / c->band_rows;
+  for (int b = c->rank; b < nb; b += c->nranks) rows += std::min(c->band_rows, H - b * c->band_rows);
+  return rows;
+}
+
+int EnsureBvhs(srt_context* c) {
+  const uint32_t need = std::max<uint32_t>(c->bvh_count, 1);
+  std::vector<srt_bvh_record> recs(need);
+  std::memset(recs.data(), 0, sizeof(srt_bvh_record) * need);   // bvhs[i >= n] read as zeros
+  for (uint32_t i = 0; i < need && i < c->h_bvhs.size(); ++i) recs[i] = c->h_bvhs[i];
+  if (need > c->bvh_capacity) {
+    FreeDev(c->d_bvhs);
+    c->d_bvhs = nullptr;
+    HIP_OK(hipMalloc(&c->d_bvhs, sizeof(srt_bvh_record) * need));
+    c->bvh_capacity = need;
+  }
+  HIP_OK(hipMemcpyAsync(c->d_bvhs, recs.data(), sizeof(srt_bvh_record) * need, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  return SRT_OK;
+}
+
+int EnsureLights(srt_context* c) {
+  if (!c->lights_dirty) return SRT_OK;
+  // the uploaded records plus one zero record that out-of-range indices map
+  // to (lights[lightCount] is an out-of-bounds SSBO read, src/main.cpp:690)
+  const size_t n = c->h_lights.size() + 1;
+  std::vector<float4> rec(2 * n, make_float4(0, 0, 0, 0));
+  for (size_t i = 0; i < c->h_lights.size(); ++i) {
+    const srt_light& l = c->h_lights[i];
+    rec[2 * i] = make_float4(l.position[0], l.position[1], l.position[2], l.intensity);
+    rec[2 * i + 1] = make_float4(l.color[0], l.color[1], l.color[2], 0.0f);
+  }
+  if (n > c->light_capacity) {
+    FreeDev(c->d_lights);
+    c->d_lights = nullptr;
+    HIP_OK(hipMalloc(&c->d_lights, sizeof(float4) * 2 * n));
+    c->light_capacity = (uint32_t)n;
+  }
+  HIP_OK(hipMemcpyAsync(c->d_lights, rec.data(), sizeof(float4) * 2 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  c->lights_dirty = false;
+  return SRT_OK;
+}
+
+// GetCamera (raytrace_compute.glsl:47-76) with focusDist = 1 (:384)
+void CameraParams(const srt_context* c, srt::KParams* kp) {
+  const float aspect = (float)c->W / (float)c->H;
+  const float hf = (float)c->W / aspect;
+  int height = (hf != hf) ? 0 : (int)hf;
+  height = (height < 1) ? 1 : height;
+  const float focus = 1.0f;
+  const float w[3] = {-c->cam_dir[0], -c->cam_dir[1], -c->cam_dir[2]};
+  float du[3], dv[3], p00[3];
+  for (int i = 0; i < 3; ++i) {
+    const float viewU = c->cam_right[i] * focus;
+    const float viewV = c->cam_up[i] * focus;
+    du[i] = viewU / (float)c->W;
+    dv[i] = viewV / (float)height;
+    const float ll = ((c->cam_origin[i] - focus * w[i]) - viewU / 2.0f) - viewV / 2.0f;
+    p00[i] = ll + 0.5f * (du[i] + dv[i]);
+  }
+  kp->cx = c->cam_origin[0]; kp->cy = c->cam_origin[1]; kp->cz = c->cam_origin[2];
+  kp->p00x = p00[0]; kp->p00y = p00[1]; kp->p00z = p00[2];
+  kp->dux = du[0]; kp->duy = du[1]; kp->duz = du[2];
+  kp->dvx = dv[0]; kp->dvy = dv[1]; kp->dvz = dv[2];
+}
+
+int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
+  if (c->W <= 0 || c->H <= 0) { srt::SetError("Width/Height not set"); return SRT_ERR_STATE; }
+  if (c->show_model && !c->scene_ok) { srt::SetError("showModel set but no scene uploaded"); return SRT_ERR_STATE; }
+  if (need_images) {
+    if (c->noise_texels != (size_t)c->W * (size_t)c->H) {
+      srt::SetError("noise buffers must hold Width*Height texels");
+      return SRT_ERR_STATE;
+    }
+    if (!c->d_accum || c->img_w != c->W || c->img_rows != LocalRows(c, c->H)) {
+      srt::SetError("images not allocated for the current Width/Height/tiling (srt_alloc_images)");
+      return SRT_ERR_STATE;
+    }
+  }
+  int rc = EnsureLights(c);
+  if (rc) return rc;
+  if (c->show_model) {
+    rc = EnsureBvhs(c);
+    if (rc) return rc;
+  }
+  std::memset(kp, 0, sizeof(*kp));
+  kp->nodes = c->d_nodes;
+  kp->tris = c->d_tris;
+  kp->mats = c->d_mats;
+  kp->lights = c->d_lights;
+  kp->bvhs = c->d_bvhs;
+  kp->noise_xy = c->d_noise_xy;
+  kp->noise_u = c->d_noise_u;
+  kp->accum = c->d_accum;
+  kp->out = c->d_out;
+  kp->stats = c->d_stats;
+  kp->W = c->W;
+  kp->H = c->H;
+  kp->WH = c->W * c->H;
+  kp->light_count = std::max(c->light_count, 0);
+  kp->light_records = (int)c->h_lights.size();
+  kp->bvh_count = c->bvh_count;
+  kp->show_model = c->show_model;
+  kp->max_depth = c->max_depth;
+  kp->rank = c->rank;
+  kp->nranks = c->nranks;
+  kp->band_rows = c->band_rows;
+  kp->local_rows = LocalRows(c, c->H);
+  kp->ext_w = c->W;
+  kp->ext_h = c->H;
+  kp->stack_entries = c->stack_entries;
+  CameraParams(c, kp);
+  return SRT_OK;
+}
+
+int Launch(srt_context* c, srt::KParams& kp, bool count) {
+  const int block = 256;
+  const size_t lds = (size_t)block * 3 * sizeof(uint32_t) * (size_t)kp.stack_entries;
+  dim3 grid((kp.W + 15) / 16, (kp.local_rows + 15) / 16);
+  if (grid.x == 0 || grid.y == 0) return SRT_OK;
+  if (count) {
+    HIP_OK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_N, c->stream));
+    hipLaunchKernelGGL(srt::pathtrace_kernel<true>, grid, dim3(block), lds, c->stream, kp);
+  } else {
+    hipLaunchKernelGGL(srt::pathtrace_kernel<false>, grid, dim3(block), lds, c->stream, kp);
+  }
+  HIP_OK(hipGetLastError());
+  if (count) {
+    unsigned long long s[srt::ST_N];
+    HIP_OK(hipMemcpyAsync(s, c->d_stats, sizeof(s), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    c->stats.rays += s[srt::ST_RAYS];
+    c->stats.nodes += s[srt::ST_NODES];
+    c->stats.tris += s[srt::ST_TRIS];
+    c->stats.rng_u += s[srt::ST_RNGU];
+    c->stats.rng_sq += s[srt::ST_RNGSQ];
+    c->stats.light_reads += s[srt::ST_LIGHTS];
+    c->stats.mat_reads += s[srt::ST_MATS];
+    c->stats.samples += s[srt::ST_SAMPLES];
+    c->stats.stack_overflow += s[srt::ST_OVERFLOW];
+    c->stats.max_stack = std::max<uint64_t>(c->stats.max_stack, s[srt::ST_MAXSTACK]);
+  }
+  return SRT_OK;
+}
+
+// Depth of each BVH (root depth 0) and index validation.
+int ValidateNodes(const srt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_tris, const srt_bvh_record* bvhs,
+                  uint32_t n_bvhs, int* max_depth) {
+  *max_depth = 0;
+  std::vector<std::pair<uint32_t, int>> st;
+  std::vector<uint8_t> seen(n_nodes, 0);
+  for (uint32_t b = 0; b < n_bvhs; ++b) {
+    if (bvhs[b].first_index >= n_nodes) {
+      srt::SetError("BVH first_index out of range");
+      return SRT_ERR_INVALID;
+    }
+    st.push_back({bvhs[b].first_index, 0});
+    while (!st.empty()) {
+      auto [i, d] = st.back();
+      st.pop_back();
+      *max_depth = std::max(*max_depth, d);
+      const srt_bvh_node& n = nodes[i];
+      if (n.prim_count > 0) {
+        if ((uint64_t)n.first_child_or_prim_index + n.prim_count > n_tris) {
+          srt::SetError("BVH leaf references triangles out of range");
+          return SRT_ERR_INVALID;
+        }
+      } else {
+        if ((uint64_t)n.first_child_or_prim_index + 1 >= n_nodes || seen[i]) {
+          srt::SetError("BVH internal node references children out of range (or a cycle)");
+          return SRT_ERR_INVALID;
+        }
+        seen[i] = 1;
+        st.push_back({n.first_child_or_prim_index, d + 1});
+        st.push_back({n.first_child_or_prim_index + 1, d + 1});
+      }
+    }
+    std::fill(seen.begin(), seen.end(), 0);
+  }
+  return SRT_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI (context part)
+// ===========================================================================
+extern "C" {
+
+const char* srt_last_error(void) { return srt::LastError(); }
+int srt_abi_version(void) { return SRT_ABI_VERSION; }
+
+int srt_create(int device, void* stream, srt_context** out) {
+  if (!out) return SRT_ERR_INVALID;
+  HIP_OK(hipSetDevice(device));
+  auto* c = new srt_context();
+  c->device = device;
+  if (stream) {
+    c->stream = static_cast<hipStream_t>(stream);
+  } else {
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      delete c;
+      srt::SetError(std::string("hipStreamCreate: ") + hipGetErrorString(e));
+      return SRT_ERR_HIP;
+    }
+    c->own_stream = true;
+  }
+  if (hipMalloc(&c->d_stats, sizeof(unsigned long long) * srt::ST_N) != hipSuccess) {
+    if (c->own_stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    srt::SetError("hipMalloc(stats) failed");
+    return SRT_ERR_HIP;
+  }
+  *out = c;
+  return SRT_OK;
+}
+
+int srt_destroy(srt_context* c) {
+  if (!c) return SRT_ERR_INVALID;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  FreeDev(c->d_nodes); FreeDev(c->d_tris); FreeDev(c->d_mats); FreeDev(c->d_bvhs); FreeDev(c->d_lights);
+  FreeDev(c->d_noise_xy); FreeDev(c->d_noise_u); FreeDev(c->d_accum); FreeDev(c->d_out); FreeDev(c->d_stats);
+  if (c->own_stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return SRT_OK;
+}
+
+void* srt_stream(srt_context* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
+
+int srt_set_bool(srt_context* c, const char* name, int v) {
+  if (!c || !name) return SRT_ERR_INVALID;
+  const std::string n(name);
+  if (n == "resetAccumBuffer") c->reset = v ? 1 : 0;
+  else if (n == "showModel") c->show_model = v ? 1 : 0;
+  else return SRT_ERR_NOT_FOUND;
+  return SRT_OK;
+}
+
+int srt_set_int(srt_context* c, const char* name, int v) {
+  if (!c || !name) return SRT_ERR_INVALID;
+  const std::string n(name);
+  if (n == "Width") c->W = v;
+  else if (n == "Height") c->H = v;
+  else if (n == "accumFrames") c->accum_frames = v;
+  else if (n == "lightCount") c->light_count = v;
+  else if (n == "maxDepth") c->max_depth = v;
+  else if (n == "resetAccumBuffer" || n == "showModel") return srt_set_bool(c, name, v);
+  else if (n == "bvh_count") c->bvh_count = (uint32_t)v;
+  else return SRT_ERR_NOT_FOUND;
+  return SRT_OK;
+}
+
+int srt_set_uint(srt_context* c, const char* name, uint32_t v) {
+  if (!c || !name) return SRT_ERR_INVALID;
+  if (std::string(name) == "bvh_count") {
+    c->bvh_count = v;
+    return SRT_OK;
+  }
+  return srt_set_int(c, name, (int)v);
+}
+
+int srt_set_float(srt_context* c, const char* name, float v) {
+  if (!c || !name) return SRT_ERR_INVALID;
+  (void)v;
+  return SRT_ERR_NOT_FOUND;  // the kernel declares no float uniforms
+}
+
+int srt_set_vec3(srt_context* c, const char* name, float x, float y, float z) {
+  if (!c || !name) return SRT_ERR_INVALID;
+  const std::string n(name);
+  float* dst = nullptr;
+  if (n == "cameraOrigin") dst = c->cam_origin;
+  else if (n == "cameraDirection") dst = c->cam_dir;
+  else if (n == "cameraUp") dst = c->cam_up;
+  else if (n == "cameraRight") dst = c->cam_right;
+  else return SRT_ERR_NOT_FOUND;
+  dst[0] = x; dst[1] = y; dst[2] = z;
+  return SRT_OK;
+}
+
+int srt_set_tiling(srt_context* c, int rank, int nranks, int band_rows) {
+  if (!c || nranks < 1 || rank < 0 || rank >= nranks || band_rows < 1) return SRT_ERR_INVALID;
+  c->rank = rank;
+  c->nranks = nranks;
+  c->band_rows = band_rows;
+  return SRT_OK;
+}
+
+int srt_local_rows(srt_context* c) { return c ? LocalRows(c, c->H) : -1; }
+
+int srt_dispatch(srt_context* c, uint32_t gx, uint32_t gy) {
+  if (!c) return SRT_ERR_INVALID;
+  HIP_OK(hipSetDevice(c->device));
+  srt::KParams kp;
+  int rc = FillParams(c, &kp, true);
+  if (rc) return rc;
+  kp.ext_w = (int)std::min<uint64_t>((uint64_t)gx * 8, (uint64_t)c->W);
+  kp.ext_h = (int)std::min<uint64_t>((uint64_t)gy * 8, (uint64_t)c->H);
+  kp.frame_first = c->accum_frames;
+  kp.nframes = 1;
+  kp.write_output = 1;
+  kp.reset = c->reset;
+  if (!kp.reset && c->accum_frames == 0) {
+    srt::SetError("accumFrames must be >= 1 for a sampling dispatch (the reference increments it first)");
+    return SRT_ERR_STATE;
+  }
+  return Launch(c, kp, false);
+}
+
+int srt_render_frames(srt_context* c, int frame_first, int nframes, int write_output, int count) {
+  if (!c || nframes < 0 || frame_first < 1) return SRT_ERR_INVALID;
+  HIP_OK(hipSetDevice(c->device));
+  srt::KParams kp;
+  int rc = FillParams(c, &kp, true);
+  if (rc) return rc;
+  if (nframes == 0) return SRT_OK;
+  kp.frame_first = frame_first;
+  kp.nframes = nframes;
+  kp.write_output = write_output ? 1 : 0;
+  kp.reset = 0;
+  return Launch(c, kp, count != 0);
+}
+
+int srt_finish(srt_context* c) {
+  if (!c) return SRT_ERR_INVALID;
+  HIP_OK(hipStreamSynchronize(c->stream));
+  return SRT_OK;
+}
+
+int srt_get_stats(srt_context* c, srt_stats* out) {
+  if (!c || !out) return SRT_ERR_INVALID;
+  *out = c->stats;
+  return SRT_OK;
+}
+
+int srt_reset_stats(srt_context* c) {
+  if (!c) return SRT_ERR_INVALID;
+  c->stats = srt_stats{};
+  return SRT_OK;
+}
+
+int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs, const srt_bvh_node* nodes,
+                     uint32_t n_nodes, const srt_material_obj* mats, const float* tex_albedo, uint32_t n_mats,
+                     const srt_triangle* tris, uint32_t n_tris, const srt_vertex* verts, uint32_t n_verts) {
+  if (!c || (n_bvhs && !bvhs) || (n_nodes && !nodes) || (n_mats && !mats) || (n_tris && !tris) ||
+      (n_verts && !verts))
+    return SRT_ERR_INVALID;
+  if (n_nodes == 0 || n_bvhs == 0) {
+    srt::SetError("scene needs at least one BVH and one node");
+    return SRT_ERR_INVALID;
+  }
+  int depth = 0;
+  int rc = ValidateNodes(nodes, n_nodes, n_tris, bvhs, n_bvhs, &depth);
+  if (rc) return rc;
+  HIP_OK(hipSetDevice(c->device));
+  // nodes: 32-B records behind a 32-B pad so sibling pairs are 64-B aligned
+  std::vector<float4> hn(2 * ((size_t)n_nodes + 1));
+  hn[0] = hn[1] = make_float4(0, 0, 0, 0);
+  for (uint32_t i = 0; i < n_nodes; ++i) {
+    const srt_bvh_node& n = nodes[i];
+    float w0, w1;
+    std::memcpy(&w0, &n.first_child_or_prim_index, 4);
+    std::memcpy(&w1, &n.prim_count, 4);
+    hn[2 * (size_t)i + 2] = make_float4(n.min_bounds[0], n.min_bounds[1], n.min_bounds[2], w0);
+    hn[2 * (size_t)i + 3] = make_float4(n.max_bounds[0], n.max_bounds[1], n.max_bounds[2], w1);
+  }
+  // materials -> shading materials (raytrace_utils.glsl:140-175); one zero
+  // record appended for out-of-range material indices (OOB SSBO reads = 0)
+  std::vector<float4> hm(2 * ((size_t)n_mats + 1), make_float4(0, 0, 0, 0));
+  for (uint32_t i = 0; i <= n_mats; ++i) {
+    srt_material_obj m{};
+    if (i < n_mats) m = mats[i];
+    float alb[3] = {m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+    if (m.use_texture) {
+      for (int k = 0; k < 3; ++k) alb[k] = tex_albedo ? tex_albedo[3 * (size_t)i + k] : 0.0f;
+    }
+    const float rough = 1.0f / (m.specular_ex + 0.0000001f);
+    hm[2 * (size_t)i] = make_float4(alb[0], alb[1], alb[2], rough);
+    hm[2 * (size_t)i + 1] = make_float4(m.specular[0], m.specular[1], m.specular[2], 0.0f);
+  }
+  // triangles: v0, e1 = v1 - v0, e2 = v2 - v0, material
+  std::vector<float4> ht(3 * (size_t)std::max<uint32_t>(n_tris, 1), make_float4(0, 0, 0, 0));
+  auto vert = [&](uint32_t i, int k) -> float { return i < n_verts ? verts[i].vertex[k] : 0.0f; };
+  for (uint32_t t = 0; t < n_tris; ++t) {
+    const srt_triangle& tr = tris[t];
+    float v0[3], e1[3], e2[3];
+    for (int k = 0; k < 3; ++k) {
+      v0[k] = vert(tr.v0_idx, k);
+      e1[k] = vert(tr.v1_idx, k) - v0[k];
+      e2[k] = vert(tr.v2_idx, k) - v0[k];
+    }
+    const uint32_t mi = tr.material_idx < n_mats ? tr.material_idx : n_mats;
+    float mf;
+    std::memcpy(&mf, &mi, 4);
+    ht[3 * (size_t)t + 0] = make_float4(v0[0], v0[1], v0[2], e1[0]);
+    ht[3 * (size_t)t + 1] = make_float4(e1[1], e1[2], e2[0], e2[1]);
+    ht[3 * (size_t)t + 2] = make_float4(e2[2], mf, 0.0f, 0.0f);
+  }
+  FreeDev(c->d_nodes); FreeDev(c->d_mats); FreeDev(c->d_tris);
+  c->d_nodes = nullptr; c->d_mats = nullptr; c->d_tris = nullptr;
+  c->scene_ok = false;
+  HIP_OK(hipMalloc(&c->d_nodes, hn.size() * sizeof(float4)));
+  HIP_OK(hipMalloc(&c->d_mats, hm.size() * sizeof(float4)));
+  HIP_OK(hipMalloc(&c->d_tris, ht.size() * sizeof(float4)));
+  HIP_OK(hipMemcpyAsync(c->d_nodes, hn.data(), hn.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipMemcpyAsync(c->d_mats, hm.data(), hm.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipMemcpyAsync(c->d_tris, ht.data(), ht.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  c->h_bvhs.assign(bvhs, bvhs + n_bvhs);
+  c->n_nodes = n_nodes;
+  c->n_tris = n_tris;
+  c->n_mats = n_mats;
+  c->stack_entries = depth + 1;
+  c->scene_ok = true;
+  if (c->bvh_count == 0) c->bvh_count = n_bvhs;
+  // the zero records beyond n_bvhs traverse from node 0 with a zero ray
+  // (raytrace_compute.glsl:144-147 reading bvhs[i] out of bounds)
+  return SRT_OK;
+}
+
+int srt_update_model_matrix(srt_context* c, uint32_t index, const float frame[16]) {
+  if (!c || !frame) return SRT_ERR_INVALID;
+  if (index >= c->h_bvhs.size()) {
+    srt::SetError("UpdateModelMatrix: index out of range");  // std::vector::at throws
+    return SRT_ERR_INVALID;
+  }
+  std::memcpy(c->h_bvhs[index].frame, frame, sizeof(float) * 16);
+  return SRT_OK;  // pushed to the device at the next launch (EnsureBvhs)
+}
+
+int srt_set_lights(srt_context* c, const srt_light* lights, uint32_t n) {
+  if (!c || (n && !lights)) return SRT_ERR_INVALID;
+  c->h_lights.assign(lights, lights + n);
+  c->lights_dirty = true;
+  return SRT_OK;
+}
+
+int srt_set_noise(srt_context* c, const float* noise_rgb, const float* noise_u_rgb, size_t texels) {
+  if (!c || !noise_rgb || !noise_u_rgb || texels == 0) return SRT_ERR_INVALID;
+  HIP_OK(hipSetDevice(c->device));
+  std::vector<float2> xy(texels);
+  std::vector<float> u(texels);
+  for (size_t i = 0; i < texels; ++i) {
+    xy[i] = make_float2(noise_rgb[3 * i], noise_rgb[3 * i + 1]);
+    u[i] = noise_u_rgb[3 * i];
+  }
+  if (texels != c->noise_texels) {
+    FreeDev(c->d_noise_xy); FreeDev(c->d_noise_u);
+    c->d_noise_xy = nullptr; c->d_noise_u = nullptr; c->noise_texels = 0;
+    HIP_OK(hipMalloc(&c->d_noise_xy, texels * sizeof(float2)));
+    HIP_OK(hipMalloc(&c->d_noise_u, texels * sizeof(float)));
+  }
+  HIP_OK(hipMemcpyAsync(c->d_noise_xy, xy.data(), texels * sizeof(float2), hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipMemcpyAsync(c->d_noise_u, u.data(), texels * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  c->noise_texels = texels;
+  return SRT_OK;
+}
+
+int srt_alloc_images(srt_context* c) {
+  if (!c || c->W <= 0 || c->H <= 0) return SRT_ERR_STATE;
+  HIP_OK(hipSetDevice(c->device));
+  const int rows = LocalRows(c, c->H);
+  const size_t px = (size_t)c->W * (size_t)std::max(rows, 1);
+  FreeDev(c->d_accum); FreeDev(c->d_out);
+  c->d_accum = nullptr; c->d_out = nullptr;
+  HIP_OK(hipMalloc(&c->d_accum, px * sizeof(float4)));
+  HIP_OK(hipMalloc(&c->d_out, px * sizeof(uint32_t)));
+  HIP_OK(hipMemsetAsync(c->d_accum, 0, px * sizeof(float4), c->stream));
+  HIP_OK(hipMemsetAsync(c->d_out, 0, px * sizeof(uint32_t), c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  c->img_w = c->W;
+  c->img_rows = rows;
+  return SRT_OK;
+}
+
+int srt_read_accum(srt_context* c, float* host, size_t bytes) {
+  if (!c || !host || !c->d_accum) return SRT_ERR_INVALID;
+  const size_t need = (size_t)c->img_w * c->img_rows * sizeof(float4);
+  if (bytes < need) return SRT_ERR_INVALID;
+  HIP_OK(hipMemcpyAsync(host, c->d_accum, need, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  return SRT_OK;
+}
+
+int srt_write_accum(srt_context* c, const float* host, size_t bytes) {
+  if (!c || !host || !c->d_accum) return SRT_ERR_INVALID;
+  const size_t need = (size_t)c->img_w * c->img_rows * sizeof(float4);
+  if (bytes < need) return SRT_ERR_INVALID;
+  HIP_OK(hipMemcpyAsync(c->d_accum, host, need, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  return SRT_OK;
+}
+
+int srt_read_output(srt_context* c, uint8_t* host, size_t bytes) {
+  if (!c || !host || !c->d_out) return SRT_ERR_INVALID;
+  const size_t need = (size_t)c->img_w * c->img_rows * sizeof(uint32_t);
+  if (bytes < need) return SRT_ERR_INVALID;
+  HIP_OK(hipMemcpyAsync(host, c->d_out, need, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  return SRT_OK;
+}
+
+int srt_image_pointers(srt_context* c, void** accum_dev, void** out_dev) {
+  if (!c) return SRT_ERR_INVALID;
+  if (accum_dev) *accum_dev = c->d_accum;
+  if (out_dev) *out_dev = c->d_out;
+  return SRT_OK;
+}
+
+int srt_trace_closest(srt_context* c, const srt_ray* rays, uint32_t n, uint32_t* hits, float* t_out) {
+  if (!c || (n && (!rays || !hits || !t_out))) return SRT_ERR_INVALID;
+  if (!c->scene_ok) { srt::SetError("no scene uploaded"); return SRT_ERR_STATE; }
+  if (n == 0) return SRT_OK;
+  HIP_OK(hipSetDevice(c->device));
+  srt::KParams kp;
+  std::memset(&kp, 0, sizeof kp);
+  int rc = EnsureBvhs(c);
+  if (rc) return rc;
+  kp.nodes = c->d_nodes;
+  kp.tris = c->d_tris;
+  kp.bvhs = c->d_bvhs;
+  kp.bvh_count = c->bvh_count;
+  kp.stack_entries = c->stack_entries;
+  kp.stats = c->d_stats;
+  srt_ray* d_rays = nullptr;
+  uint32_t* d_hits = nullptr;
+  float* d_t = nullptr;
+  HIP_OK(hipMalloc(&d_rays, sizeof(srt_ray) * n));
+  HIP_OK(hipMalloc(&d_hits, sizeof(uint32_t) * n));
+  HIP_OK(hipMalloc(&d_t, sizeof(float) * n));
+  HIP_OK(hipMemcpyAsync(d_rays, rays, sizeof(srt_ray) * n, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_N, c->stream));
+  const int block = 256;
+  const size_t lds = (size_t)block * 3 * sizeof(uint32_t) * (size_t)kp.stack_entries;
+  hipLaunchKernelGGL(srt::closest_kernel, dim3((n + block - 1) / block), dim3(block), lds, c->stream, kp, d_rays, n,
+                     d_hits, d_t);
+  HIP_OK(hipGetLastError());
+  unsigned long long s[srt::ST_N];
+  HIP_OK(hipMemcpyAsync(hits, d_hits, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipMemcpyAsync(t_out, d_t, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipMemcpyAsync(s, c->d_stats, sizeof(s), hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  c->stats.rays += n;
+  c->stats.nodes += s[srt::ST_NODES];
+  c->stats.tris += s[srt::ST_TRIS];
+  (void)hipFree(d_rays);
+  (void)hipFree(d_hits);
+  (void)hipFree(d_t);
+  return SRT_OK;
+}
+
+}  // extern "C"

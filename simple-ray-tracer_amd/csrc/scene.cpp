@@ -1,0 +1,527 @@
+// scene.cpp -- scene producers: OBJ/MTL reader, midpoint-split BVH, flattening.
+//
+// Clean-room restatement of the reference's input producers, reproducing
+// their output arrays bit for bit (SURVEY.md 8a "Host-side inputs"):
+//   src/asset_utils/model_loader.cpp:20-365   (LoadObject / ParseOBJ / ParseMTL /
+//                                               ConvertCPUGeometryToModel)
+//   include/intersection_utils/bvh.h:40-148    (BVH ctor, UpdateNodeBounds, Subdivide)
+//   src/asset_utils/gpu_loader.cpp:63-133      (UploadModelDataToGPU flattening)
+// All float arithmetic is plain IEEE fp32 in source order (the reference is
+// built by g++ for x86-64 without -march, so SSE and no FMA contraction).
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <limits>
+#include <sstream>
+#include <unordered_map>
+#include <zlib.h>
+
+#include "srt_internal.hpp"
+
+namespace srt {
+
+namespace {
+
+const char* kWs = " \n\r\t";
+
+void Trim(std::string* line) {
+  line->erase(0, line->find_first_not_of(kWs));
+  const auto last = line->find_last_not_of(kWs);
+  line->erase(last == std::string::npos ? 0 : last + 1);
+}
+
+// istream >> float: leading whitespace skipped, longest valid prefix parsed.
+bool ReadFloat(std::istringstream& ls, float* out) {
+  std::string tok;
+  if (!(ls >> tok)) return false;
+  const char* s = tok.c_str();
+  char* end = nullptr;
+  errno = 0;
+  float v = std::strtof(s, &end);
+  if (end == s) return false;
+  *out = v;
+  return true;
+}
+
+struct Face {
+  uint32_t v[3];
+};
+
+struct SubGeometry {
+  std::string material;
+  std::vector<Face> faces;
+};
+
+// model_loader.cpp:35-177 ParseOBJ
+bool ParseOBJ(const std::string& path, std::vector<Vec3>* vertices, std::vector<SubGeometry>* geos,
+              std::vector<std::string>* mtl_files, uint64_t* dropped, std::string* err) {
+  std::ifstream file(path);
+  if (!file) {
+    *err = "cannot open " + path;
+    return false;
+  }
+  SubGeometry cur;
+  std::string line;
+  while (std::getline(file, line)) {
+    Trim(&line);
+    if (line.empty() || line[0] == '#') continue;
+    std::istringstream ls(line);
+    std::string prefix;
+    ls >> prefix;
+    if (prefix == "v") {
+      Vec3 v;
+      if (ReadFloat(ls, &v.x) && ReadFloat(ls, &v.y) && ReadFloat(ls, &v.z)) vertices->push_back(v);
+    } else if (prefix == "f") {
+      std::vector<uint32_t> vi;
+      std::string tok;
+      while (ls >> tok) {
+        const auto slash = tok.find('/');
+        const std::string v = tok.substr(0, slash);
+        if (!v.empty()) {
+          char* end = nullptr;
+          long idx = std::strtol(v.c_str(), &end, 10);
+          if (end == v.c_str()) {
+            *err = "bad face index '" + v + "' in " + path;
+            return false;  // std::stol throws in the reference
+          }
+          vi.push_back(static_cast<uint32_t>(idx - 1));  // OBJ indices are 1-based
+        }
+      }
+      if (vi.size() != 3 && vi.size() != 4) {
+        ++*dropped;  // "Unexpected face vertex count" (model_loader.cpp:110-113)
+        continue;
+      }
+      cur.faces.push_back(Face{{vi[0], vi[1], vi[2]}});
+      if (vi.size() == 4) cur.faces.push_back(Face{{vi[0], vi[2], vi[3]}});
+    } else if (prefix == "usemtl") {
+      if (!cur.material.empty()) {
+        geos->push_back(std::move(cur));
+        cur = SubGeometry();
+      }
+      std::string name;
+      ls >> name;
+      cur.material = name;
+    } else if (prefix == "mtllib") {
+      std::string name;
+      ls >> name;
+      mtl_files->push_back(name);
+    }
+    // vt / vn are parsed by the reference but never reach the GPU (has_texcoords
+    // is never set, types.h:105); s / o / g and unknown prefixes are ignored.
+  }
+  if (!cur.material.empty()) geos->push_back(std::move(cur));
+  else *dropped += cur.faces.size();  // trailing faces without a material are dropped
+  return true;
+}
+
+// model_loader.cpp:179-278 ParseMTL.  Materials keep first-definition order
+// (the reference's unordered_map order is renderer-invisible).
+void ParseMTL(const std::string& folder, const std::string& file_name, std::vector<std::string>* names,
+              std::vector<Material>* mats) {
+  std::ifstream file(folder + file_name);
+  if (!file) return;  // "Cannot open file" and continue
+  long current = -1;
+  std::string line;
+  while (std::getline(file, line)) {
+    Trim(&line);
+    if (line.empty() || line[0] == '#') continue;
+    std::istringstream ls(line);
+    std::string prefix;
+    ls >> prefix;
+    if (prefix == "newmtl") {
+      std::string name;
+      ls >> name;
+      bool dup = false;
+      for (const auto& n : *names) dup |= (n == name);
+      if (!dup) {  // a duplicate name leaves `current` on the previous material
+        names->push_back(name);
+        mats->emplace_back();
+        current = static_cast<long>(mats->size()) - 1;
+      }
+      continue;
+    }
+    if (current < 0) continue;
+    Material& m = (*mats)[current];
+    if (prefix == "map_Kd") {
+      std::string tex;
+      ls >> tex;
+      m.use_texture = true;
+      m.texture_path = folder + "/" + tex;
+    } else if (prefix == "Kd") {
+      Vec3 d;
+      ReadFloat(ls, &d.x) && ReadFloat(ls, &d.y) && ReadFloat(ls, &d.z);
+      m.diffuse = d;
+    } else if (prefix == "Ks") {
+      Vec3 s;
+      ReadFloat(ls, &s.x) && ReadFloat(ls, &s.y) && ReadFloat(ls, &s.z);
+      m.specular = s;
+    } else if (prefix == "Ns") {
+      float e = 0.f;
+      ReadFloat(ls, &e);
+      m.specular_ex = e;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// BVH (bvh.h:40-148) over triangles, with model_loader.cpp:333-352 centre/bounds
+// ---------------------------------------------------------------------------
+class BvhBuilder {
+ public:
+  BvhBuilder(Model* m) : m_(m) {}
+
+  void Build() {
+    const size_t n = m_->prims.size();
+    idx_.resize(n);
+    for (size_t i = 0; i < n; ++i) idx_[i] = static_cast<uint32_t>(i);
+    centers_.resize(n);
+    bmin_.resize(n);
+    bmax_.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+      const Triangle& t = m_->prims[i];
+      const Vec3 p0 = Pos(t.vertex_idxs[0]), p1 = Pos(t.vertex_idxs[1]), p2 = Pos(t.vertex_idxs[2]);
+      // (p0 + p1 + p2) / 3.0f
+      centers_[i] = Vec3((p0.x + p1.x + p2.x) / 3.0f, (p0.y + p1.y + p2.y) / 3.0f, (p0.z + p1.z + p2.z) / 3.0f);
+      Vec3 lo = vmin(vmin(p0, p1), p2);
+      Vec3 hi = vmax(vmax(p0, p1), p2);
+      bmin_[i] = lo;
+      bmax_[i] = hi;
+    }
+    nodes_.assign(n == 0 ? 1 : 2 * n - 1, BVHNode());
+    next_ = 1;
+    BVHNode& root = nodes_[0];
+    root.first_child = 0;
+    root.first_prim_index = 0;
+    root.prim_count = static_cast<uint32_t>(n);
+    UpdateBounds(0);
+    // iterative DFS that visits nodes in the recursive order (left, then right)
+    struct Item { uint32_t node; uint32_t depth; };
+    std::vector<Item> stack{{0, 0}};
+    uint32_t max_depth = 0, leaves = 0;
+    while (!stack.empty()) {
+      Item it = stack.back();
+      stack.pop_back();
+      if (it.depth > max_depth) max_depth = it.depth;
+      uint32_t l = 0;
+      if (Subdivide(it.node, &l)) {
+        stack.push_back({l + 1, it.depth + 1});
+        stack.push_back({l, it.depth + 1});
+      } else {
+        ++leaves;
+      }
+    }
+    nodes_.resize(next_);
+    std::vector<Triangle> np;
+    np.reserve(n);
+    for (uint32_t i : idx_) np.push_back(m_->prims[i]);
+    m_->prims = std::move(np);
+    m_->nodes = std::move(nodes_);
+    m_->max_depth = max_depth;
+    m_->leaves = leaves;
+  }
+
+ private:
+  Vec3 Pos(uint32_t v) const {
+    const srt_vertex& sv = m_->vertices[v];
+    return Vec3(sv.vertex[0], sv.vertex[1], sv.vertex[2]);
+  }
+
+  // bvh.h:80-96
+  void UpdateBounds(uint32_t ni) {
+    BVHNode& node = nodes_[ni];
+    node.min_bounds = Vec3(std::numeric_limits<float>::max(), std::numeric_limits<float>::max(),
+                           std::numeric_limits<float>::max());
+    node.max_bounds = Vec3(std::numeric_limits<float>::lowest(), std::numeric_limits<float>::lowest(),
+                           std::numeric_limits<float>::lowest());
+    for (uint32_t i = 0; i < node.prim_count; ++i) {
+      const uint32_t p = idx_[node.first_prim_index + i];
+      node.min_bounds = vmin(node.min_bounds, bmin_[p]);
+      node.max_bounds = vmax(node.max_bounds, bmax_[p]);
+    }
+  }
+
+  // bvh.h:98-148 (children are expanded by the caller, left first)
+  bool Subdivide(uint32_t ni, uint32_t* left_out) {
+    BVHNode& node = nodes_[ni];
+    if (node.prim_count <= 2) return false;
+    const Vec3 extent(node.max_bounds.x - node.min_bounds.x, node.max_bounds.y - node.min_bounds.y,
+                      node.max_bounds.z - node.min_bounds.z);
+    int axis = 0;
+    if (extent.y > extent.x) axis = 1;
+    if (extent.z > extent[axis]) axis = 2;
+    const float split = node.min_bounds[axis] + extent[axis] * 0.5f;
+    uint32_t i = node.first_prim_index;
+    uint32_t j = i + node.prim_count - 1;
+    while (i <= j && j != static_cast<uint32_t>(-1)) {
+      if (centers_[idx_[i]][axis] < split) {
+        i++;
+      } else {
+        std::swap(idx_[i], idx_[j]);
+        j--;
+      }
+    }
+    const uint32_t left_count = i - node.first_prim_index;
+    if (left_count == 0 || left_count == node.prim_count) return false;
+    const uint32_t l = next_, r = next_ + 1;
+    node.first_child = l;
+    nodes_[l].first_prim_index = node.first_prim_index;
+    nodes_[l].prim_count = left_count;
+    nodes_[r].first_prim_index = i;
+    nodes_[r].prim_count = node.prim_count - left_count;
+    node.prim_count = 0;
+    next_ += 2;
+    UpdateBounds(l);
+    UpdateBounds(r);
+    *left_out = l;
+    return true;
+  }
+
+  Model* m_;
+  std::vector<uint32_t> idx_;
+  std::vector<Vec3> centers_, bmin_, bmax_;
+  std::vector<BVHNode> nodes_;
+  uint32_t next_ = 0;
+};
+
+// ---------------------------------------------------------------------------
+// Minimal PNG reader (8-bit, non-interlaced) for map_Kd textures.
+// ---------------------------------------------------------------------------
+uint32_t Be32(const unsigned char* p) {
+  return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | uint32_t(p[3]);
+}
+
+bool DecodePng(const std::string& path, int* w, int* h, int* ch, std::vector<unsigned char>* px,
+               std::string* err) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) { *err = "cannot open texture " + path; return false; }
+  std::vector<unsigned char> d((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  static const unsigned char sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+  if (d.size() < 8 || std::memcmp(d.data(), sig, 8) != 0) { *err = "not a PNG: " + path; return false; }
+  size_t pos = 8;
+  int bitdepth = 0, ctype = 0, interlace = 0;
+  std::vector<unsigned char> idat, plte, trns;
+  while (pos + 12 <= d.size()) {
+    const uint32_t len = Be32(&d[pos]);
+    const std::string type(reinterpret_cast<const char*>(&d[pos + 4]), 4);
+    if (pos + 12 + len > d.size()) break;
+    const unsigned char* body = &d[pos + 8];
+    if (type == "IHDR") {
+      *w = static_cast<int>(Be32(body));
+      *h = static_cast<int>(Be32(body + 4));
+      bitdepth = body[8];
+      ctype = body[9];
+      interlace = body[12];
+    } else if (type == "PLTE") {
+      plte.assign(body, body + len);
+    } else if (type == "tRNS") {
+      trns.assign(body, body + len);
+    } else if (type == "IDAT") {
+      idat.insert(idat.end(), body, body + len);
+    } else if (type == "IEND") {
+      break;
+    }
+    pos += 12 + len;
+  }
+  if (bitdepth != 8 || interlace != 0) { *err = "unsupported PNG (bit depth/interlace): " + path; return false; }
+  int in_ch = ctype == 0 ? 1 : ctype == 2 ? 3 : ctype == 3 ? 1 : ctype == 4 ? 2 : ctype == 6 ? 4 : 0;
+  if (in_ch == 0) { *err = "unsupported PNG colour type: " + path; return false; }
+  const size_t stride = size_t(*w) * in_ch;
+  std::vector<unsigned char> raw((stride + 1) * size_t(*h));
+  uLongf rawlen = raw.size();
+  if (uncompress(raw.data(), &rawlen, idat.data(), idat.size()) != Z_OK || rawlen != raw.size()) {
+    *err = "PNG inflate failed: " + path;
+    return false;
+  }
+  std::vector<unsigned char> img(stride * size_t(*h));
+  for (int y = 0; y < *h; ++y) {
+    const unsigned char ft = raw[y * (stride + 1)];
+    const unsigned char* src = &raw[y * (stride + 1) + 1];
+    unsigned char* dst = &img[y * stride];
+    const unsigned char* up = y > 0 ? &img[(y - 1) * stride] : nullptr;
+    for (size_t x = 0; x < stride; ++x) {
+      const int a = x >= size_t(in_ch) ? dst[x - in_ch] : 0;
+      const int b = up ? up[x] : 0;
+      const int c = (up && x >= size_t(in_ch)) ? up[x - in_ch] : 0;
+      int v = src[x];
+      switch (ft) {
+        case 0: break;
+        case 1: v += a; break;
+        case 2: v += b; break;
+        case 3: v += (a + b) / 2; break;
+        case 4: {
+          const int p = a + b - c, pa = std::abs(p - a), pb = std::abs(p - b), pc = std::abs(p - c);
+          v += (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
+          break;
+        }
+        default: *err = "bad PNG filter: " + path; return false;
+      }
+      dst[x] = static_cast<unsigned char>(v & 0xFF);
+    }
+  }
+  if (ctype == 3) {  // palette -> RGB(A), as stb_image expands it
+    const int out_ch = trns.empty() ? 3 : 4;
+    px->resize(size_t(*w) * (*h) * out_ch);
+    for (size_t i = 0; i < size_t(*w) * (*h); ++i) {
+      const unsigned k = img[i];
+      for (int c = 0; c < 3; ++c) (*px)[i * out_ch + c] = (3 * k + c < plte.size()) ? plte[3 * k + c] : 0;
+      if (out_ch == 4) (*px)[i * out_ch + 3] = k < trns.size() ? trns[k] : 255;
+    }
+    *ch = out_ch;
+  } else {
+    *px = std::move(img);
+    *ch = in_ch;
+  }
+  return true;
+}
+
+}  // namespace
+
+// texture(sampler2D, vec2(0)) at level 0 with GL_REPEAT + GL_LINEAR: the four
+// corner texels, weight 1/4 each (gpu_texture.h:24-68 uploads stb_image rows).
+bool DecodeTextureCornerAlbedo(const std::string& path, Vec3* out, std::string* err) {
+  int w = 0, h = 0, ch = 0;
+  std::vector<unsigned char> px;
+  if (!DecodePng(path, &w, &h, &ch, &px, err)) return false;
+  auto texel = [&](int x, int y) -> Vec3 {
+    const unsigned char* p = &px[(size_t(y) * w + x) * ch];
+    // GL_RED (1 ch) samples as (r,0,0); 2-channel falls back to GL_RGB in the
+    // reference's format switch, reading (r,g,?) -- treated as (r,g,0).
+    float r = p[0] / 255.0f;
+    float g = ch >= 2 ? p[1] / 255.0f : 0.0f;
+    float b = ch >= 3 ? p[2] / 255.0f : 0.0f;
+    return Vec3(r, g, b);
+  };
+  const Vec3 a = texel(0, 0), b = texel(w - 1, 0), c = texel(0, h - 1), d = texel(w - 1, h - 1);
+  *out = Vec3(0.25f * (((a.x + b.x) + c.x) + d.x), 0.25f * (((a.y + b.y) + c.y) + d.y),
+              0.25f * (((a.z + b.z) + c.z) + d.z));
+  return true;
+}
+
+void BuildBVH(Model* m) { BvhBuilder(m).Build(); }
+
+// model_loader.cpp:20-32 + 280-365
+std::unique_ptr<Model> LoadObjectFile(const std::string& obj_path, std::string* err) {
+  std::vector<Vec3> vertices;
+  std::vector<SubGeometry> geos;
+  std::vector<std::string> mtl_files;
+  auto model = std::make_unique<Model>();
+  if (!ParseOBJ(obj_path, &vertices, &geos, &mtl_files, &model->faces_dropped, err)) return nullptr;
+  const auto slash = obj_path.find_last_of('/');
+  const std::string folder = slash == std::string::npos ? std::string("./") : obj_path.substr(0, slash + 1);
+  std::vector<std::string> names;
+  for (const auto& f : mtl_files) ParseMTL(folder, f, &names, &model->materials);
+  for (auto& m : model->materials) {
+    if (m.use_texture && !DecodeTextureCornerAlbedo(m.texture_path, &m.tex_albedo, err)) return nullptr;
+  }
+  // per-corner vertex duplication (model_loader.cpp:302-331); uv stays (0,0)
+  for (const auto& g : geos) {
+    uint32_t mat = 0;
+    for (size_t k = 0; k < names.size(); ++k)
+      if (names[k] == g.material) { mat = static_cast<uint32_t>(k); break; }
+    for (const auto& f : g.faces) {
+      Triangle t;
+      t.material_idx = mat;
+      for (int c = 0; c < 3; ++c) {
+        if (f.v[c] >= vertices.size()) {
+          *err = "face references vertex " + std::to_string(f.v[c] + 1) + " out of range";
+          return nullptr;
+        }
+        const Vec3& p = vertices[f.v[c]];
+        srt_vertex sv{};
+        sv.vertex[0] = p.x; sv.vertex[1] = p.y; sv.vertex[2] = p.z;
+        model->vertices.push_back(sv);
+        t.vertex_idxs[c] = static_cast<uint32_t>(model->vertices.size() - 1);
+      }
+      model->prims.push_back(t);
+    }
+  }
+  if (model->prims.empty()) {
+    *err = "no triangles in " + obj_path;
+    return nullptr;
+  }
+  BuildBVH(model.get());
+  return model;
+}
+
+std::unique_ptr<Model> ModelFromTriangles(const float* xyz9, uint32_t n, const Vec3& kd, const Vec3& ks,
+                                          float ns) {
+  auto model = std::make_unique<Model>();
+  Material m;
+  m.diffuse = kd;
+  m.specular = ks;
+  m.specular_ex = ns;
+  model->materials.push_back(m);
+  model->vertices.resize(size_t(n) * 3);
+  model->prims.resize(n);
+  for (uint32_t t = 0; t < n; ++t) {
+    for (int c = 0; c < 3; ++c) {
+      srt_vertex& sv = model->vertices[size_t(t) * 3 + c];
+      sv = srt_vertex{};
+      sv.vertex[0] = xyz9[size_t(t) * 9 + c * 3 + 0];
+      sv.vertex[1] = xyz9[size_t(t) * 9 + c * 3 + 1];
+      sv.vertex[2] = xyz9[size_t(t) * 9 + c * 3 + 2];
+      model->prims[t].vertex_idxs[c] = t * 3 + c;
+    }
+    model->prims[t].material_idx = 0;
+  }
+  if (n > 0) BuildBVH(model.get());
+  return model;
+}
+
+// gpu_loader.cpp:63-133 (the index rebasing; uploads happen in the context)
+std::unique_ptr<Scene> FlattenModels(const std::vector<const Model*>& models, std::string* err) {
+  auto s = std::make_unique<Scene>();
+  uint32_t node_off = 0, tri_off = 0, mat_off = 0, vert_off = 0;
+  for (const Model* m : models) {
+    if (!m) {
+      *err = "Model was null!";
+      return nullptr;
+    }
+    const uint32_t model_mat_off = mat_off;
+    for (const auto& mat : m->materials) {
+      srt_material_obj g{};
+      g.diffuse[0] = mat.diffuse.x; g.diffuse[1] = mat.diffuse.y; g.diffuse[2] = mat.diffuse.z;
+      g.specular[0] = mat.specular.x; g.specular[1] = mat.specular.y; g.specular[2] = mat.specular.z;
+      g.specular_ex = mat.specular_ex;
+      g.use_texture = mat.use_texture ? 1u : 0u;
+      s->mats.push_back(g);
+      s->tex_albedo.push_back(mat.tex_albedo.x);
+      s->tex_albedo.push_back(mat.tex_albedo.y);
+      s->tex_albedo.push_back(mat.tex_albedo.z);
+    }
+    mat_off += static_cast<uint32_t>(m->materials.size());
+    const uint32_t model_vert_off = vert_off;
+    s->verts.insert(s->verts.end(), m->vertices.begin(), m->vertices.end());
+    vert_off += static_cast<uint32_t>(m->vertices.size());
+    srt_bvh_record b{};
+    b.first_index = node_off;
+    b.count = static_cast<uint32_t>(m->nodes.size());
+    for (int i = 0; i < 16; ++i) b.frame[i] = (i % 5 == 0) ? 1.0f : 0.0f;  // glm::mat4(1)
+    s->bvhs.push_back(b);
+    const uint32_t local_tri_off = tri_off;
+    for (const auto& t : m->prims) {
+      srt_triangle g;
+      g.v0_idx = t.vertex_idxs[0] + model_vert_off;
+      g.v1_idx = t.vertex_idxs[1] + model_vert_off;
+      g.v2_idx = t.vertex_idxs[2] + model_vert_off;
+      g.material_idx = t.material_idx + model_mat_off;
+      s->tris.push_back(g);
+    }
+    tri_off += static_cast<uint32_t>(m->prims.size());
+    for (const auto& n : m->nodes) {
+      srt_bvh_node g;
+      g.min_bounds[0] = n.min_bounds.x; g.min_bounds[1] = n.min_bounds.y; g.min_bounds[2] = n.min_bounds.z;
+      g.max_bounds[0] = n.max_bounds.x; g.max_bounds[1] = n.max_bounds.y; g.max_bounds[2] = n.max_bounds.z;
+      g.first_child_or_prim_index = n.prim_count > 0 ? n.first_prim_index + local_tri_off : n.first_child + node_off;
+      g.prim_count = n.prim_count;
+      s->nodes.push_back(g);
+    }
+    node_off += b.count;
+  }
+  return s;
+}
+
+}  // namespace srt

@@ -1,0 +1,94 @@
+// srt_internal.hpp -- host-side types shared by the producers, the context and
+// the C ABI.  Not part of the public interface (include/srt_amd.h is).
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/srt_amd.h"
+
+namespace srt {
+
+struct Vec3 {
+  float x = 0.f, y = 0.f, z = 0.f;
+  Vec3() = default;
+  Vec3(float a, float b, float c) : x(a), y(b), z(c) {}
+  float& operator[](int i) { return i == 0 ? x : (i == 1 ? y : z); }
+  float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+};
+
+// glm::min / glm::max component rules (glm: min(x,y) = y < x ? y : x).
+inline Vec3 vmin(const Vec3& a, const Vec3& b) {
+  return {b.x < a.x ? b.x : a.x, b.y < a.y ? b.y : a.y, b.z < a.z ? b.z : a.z};
+}
+inline Vec3 vmax(const Vec3& a, const Vec3& b) {
+  return {a.x < b.x ? b.x : a.x, a.y < b.y ? b.y : a.y, a.z < b.z ? b.z : a.z};
+}
+
+// intersection_utils/bvh.h:23-30 (host node, before GPU packing)
+struct BVHNode {
+  Vec3 min_bounds;
+  Vec3 max_bounds;
+  uint32_t first_child = 0;
+  uint32_t first_prim_index = 0;
+  uint32_t prim_count = 0;
+};
+
+// asset_utils/types.h:25-28
+struct Triangle {
+  uint32_t vertex_idxs[3];
+  uint32_t material_idx;
+};
+
+// asset_utils/types.h:31-37 (texture decoded to its uv=(0,0) sample at load)
+struct Material {
+  Vec3 diffuse;
+  Vec3 specular;
+  float specular_ex = 0.f;
+  bool use_texture = false;
+  std::string texture_path;
+  Vec3 tex_albedo;  // texture(sampler2D(handle), (0,0)).xyz
+};
+
+// asset_utils/types.h:39-52
+struct Model {
+  std::vector<BVHNode> nodes;
+  std::vector<Triangle> prims;         // BVH-ordered
+  std::vector<Material> materials;
+  std::vector<srt_vertex> vertices;    // PackedVertexData, 32 B
+  uint64_t faces_dropped = 0;
+  uint32_t max_depth = 0;
+  uint32_t leaves = 0;
+};
+
+// Flattened scene: the five SSBO arrays of gpu_loader.cpp:44-52.
+struct Scene {
+  std::vector<srt_bvh_record> bvhs;
+  std::vector<srt_bvh_node> nodes;
+  std::vector<srt_material_obj> mats;
+  std::vector<float> tex_albedo;       // 3 per material
+  std::vector<srt_triangle> tris;
+  std::vector<srt_vertex> verts;
+};
+
+// producers (scene.cpp)
+std::unique_ptr<Model> LoadObjectFile(const std::string& obj_path, std::string* err);
+std::unique_ptr<Model> ModelFromTriangles(const float* xyz9, uint32_t n, const Vec3& kd, const Vec3& ks,
+                                          float ns);
+void BuildBVH(Model* m);  // bvh.h:40-75 over m->prims with the loader's centre/bounds functions
+std::unique_ptr<Scene> FlattenModels(const std::vector<const Model*>& models, std::string* err);
+bool DecodeTextureCornerAlbedo(const std::string& path, Vec3* out, std::string* err);
+
+// noise.cpp
+void GlibcRand(uint32_t n, int32_t* out);
+void GenerateNoise(uint32_t texels, bool gcc_order, float* noise, float* noise_u);
+
+// camera.cpp
+void CameraReset(bool show_model, Vec3* origin, Vec3* front, Vec3* up, Vec3* right);
+void CameraBasis(float yaw, float pitch, Vec3* front, Vec3* up, Vec3* right);
+
+void SetError(const std::string& msg);
+
+}  // namespace srt

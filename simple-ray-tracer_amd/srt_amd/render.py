@@ -1,0 +1,149 @@
+"""Progressive renderer: the per-frame contract of src/main.cpp (:579-718) driven on the HIP kernels.
+
+The reference app resets the accumulation buffer on the first frame
+(EnableMouseCapture(false) sets the reset flag, input_handler.cpp:172), so frame
+1 is a clear (accumFrames = 1) and frame k >= 2 traces sample index
+k % (W*H).  After N sampled frames the displayed image is
+sRGB(sum_{k=2}^{N+1} L_k / (N + 1)).
+"""
+from __future__ import annotations
+
+import pathlib
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import (MODEL_LIGHTS, SPHERE_LIGHTS, Camera, Compute, Model, Scene, generate_noise, lights_array, load_obj,
+               model_from_triangles)
+
+
+@dataclass
+class FrameSetup:
+    """Everything the kernel reads, in reference layouts (also what the CPU oracle consumes)."""
+    width: int
+    height: int
+    show_model: bool
+    scene: Scene | None
+    lights: np.ndarray
+    noise: np.ndarray
+    noise_u: np.ndarray
+    camera: Camera
+    max_depth: int = 5
+    bvh_count: int = 1
+
+
+def make_setup(width: int, height: int, *, show_model: bool, models=None, lights=None, max_depth: int = 5,
+               bvh_count: int | None = None, gcc_order: bool = True, noise=None) -> FrameSetup:
+    scene = Scene.from_models(models) if (show_model and models) else None
+    if lights is None:
+        lights = MODEL_LIGHTS if show_model else SPHERE_LIGHTS
+    la = lights if isinstance(lights, np.ndarray) else lights_array(lights)
+    if noise is None:
+        noise = generate_noise(width, height, gcc_order)
+    cam = Camera(show_model)
+    if bvh_count is None:
+        bvh_count = len(scene.bvhs) if scene is not None else 0
+    return FrameSetup(width, height, show_model, scene, la, noise[0], noise[1], cam, max_depth, bvh_count)
+
+
+class Renderer:
+    """Drives one Compute context through the reference's progressive loop."""
+
+    def __init__(self, setup: FrameSetup, *, device: int = 0, stream: int | None = None, rank: int = 0,
+                 nranks: int = 1, band_rows: int = 16):
+        self.setup = setup
+        c = Compute("builtin:raytrace_compute", device=device, stream=stream).Init()
+        self.compute = c
+        c.Use()
+        c.SetInt("Width", setup.width)
+        c.SetInt("Height", setup.height)
+        c.SetBool("showModel", setup.show_model)
+        c.SetInt("maxDepth", setup.max_depth)
+        c.SetUInt("bvh_count", setup.bvh_count)
+        c.SetInt("lightCount", len(setup.lights))
+        cam = setup.camera
+        c.SetVec3("cameraOrigin", cam.getOrigin())
+        c.SetVec3("cameraDirection", cam.getForward())
+        c.SetVec3("cameraUp", cam.getUpVector())
+        c.SetVec3("cameraRight", cam.getRightVector())
+        c.bind_lights(setup.lights)
+        c.bind_noise(setup.noise, setup.noise_u)
+        if setup.scene is not None:
+            c.bind_scene(setup.scene)
+        c.set_tiling(rank, nranks, band_rows)
+        c.alloc_images()
+        self.accum_frames = 0
+
+    @property
+    def groups(self):
+        s = self.setup
+        return (s.width + 7) // 8, (s.height + 7) // 8
+
+    def clear(self):
+        """Frame 1 of the app: accumFrames = 1 with resetAccumBuffer = true."""
+        self.accum_frames = 1
+        c = self.compute
+        c.SetBool("resetAccumBuffer", True)
+        c.SetInt("accumFrames", self.accum_frames)
+        c.Dispatch(*self.groups)
+        c.SetBool("resetAccumBuffer", False)
+
+    def frame(self):
+        """One more progressive frame (one glDispatchCompute)."""
+        self.accum_frames += 1
+        c = self.compute
+        c.SetBool("resetAccumBuffer", False)
+        c.SetInt("accumFrames", self.accum_frames)
+        c.Dispatch(*self.groups)
+
+    def render(self, spp: int, *, count: bool = False, write_output: bool = True, clear: bool = True):
+        """`spp` progressive frames in one fused launch (same accumulation as `spp` Dispatch calls)."""
+        if clear:
+            self.clear()
+        first = self.accum_frames + 1
+        self.compute.render_frames(first, spp, write_output=write_output, count=count)
+        self.accum_frames += spp
+
+    def finish(self):
+        self.compute.Finish()
+
+    def accum(self) -> np.ndarray:
+        return self.compute.read_accum()
+
+    def output(self) -> np.ndarray:
+        return self.compute.read_output()
+
+    def close(self):
+        self.compute.close()
+
+
+def rubik_model(objects_dir: str | pathlib.Path) -> Model:
+    return load_obj(pathlib.Path(objects_dir) / "Rubik" / "Rubik.obj")
+
+
+def splitmix64_uniform(n: int, seed: int = 0x5EED2025) -> np.ndarray:
+    """n uniforms in [0, 1) as float32: SplitMix64 stream, top 24 bits * 2^-24."""
+    M = np.uint64(0xFFFFFFFFFFFFFFFF)
+    idx = np.arange(1, n + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (np.uint64(seed) + idx * np.uint64(0x9E3779B97F4A7C15)) & M
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return ((z >> np.uint64(40)).astype(np.float32)) * np.float32(2.0 ** -24)
+
+
+def synthetic_triangles(n_tris: int, seed: int = 0x5EED2025) -> np.ndarray:
+    """centres U([-10,10]x[0,18]x[-10,10]), vertices = centre + U(-0.05,0.05)^3."""
+    u = splitmix64_uniform(12 * n_tris, seed).reshape(n_tris, 12)
+    lo = np.array([-10.0, 0.0, -10.0], np.float32)
+    ext = np.array([20.0, 18.0, 20.0], np.float32)
+    c = lo + ext * u[:, 0:3]
+    tri = np.empty((n_tris, 3, 3), np.float32)
+    for k in range(3):
+        tri[:, k, :] = c + (np.float32(-0.05) + np.float32(0.1) * u[:, 3 + 3 * k:6 + 3 * k])
+    return tri.reshape(n_tris, 9)
+
+
+def synthetic_model(n_tris: int, seed: int = 0x5EED2025) -> Model:
+    return model_from_triangles(synthetic_triangles(n_tris, seed), kd=(0.8, 0.8, 0.8), ks=(0.0, 0.0, 0.0), ns=10.0)
