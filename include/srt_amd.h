@@ -133,6 +133,15 @@ int srt_read_output(srt_context* ctx, uint8_t* host_rgba8, size_t bytes);
 int srt_write_accum(srt_context* ctx, const float* host_rgba32f, size_t bytes);
 /* Device pointers of the images (for RCCL gathers without a host copy). */
 int srt_image_pointers(srt_context* ctx, void** accum_dev, void** out_dev);
+/* Use caller-owned device buffers (>= local_rows * Width RGBA32F / RGBA8) as
+ * image3 / image0, e.g. tensors an RCCL gather reads from. */
+int srt_set_image_buffers(srt_context* ctx, void* accum_dev, void* out_dev);
+/* Root side of the multi-GPU frame: `gathered` holds nranks blocks of
+ * rows_pad packed local rows (rank order); writes the full-frame RGBA32F
+ * accumulation image and sRGB8 image for accumFrames = `frames` (either
+ * output may be NULL).  Enqueued on the context's stream. */
+int srt_assemble_bands(srt_context* ctx, const void* gathered, int nranks, int rows_pad, int frames,
+                       void* accum_full, void* out_full);
 
 /* Closest-hit query: the test kernel ray_intersects.glsl:135-161 fed through
  * AssetUtils::UpdateRays (gpu_loader.cpp:198-210); hits[i] = triangle index

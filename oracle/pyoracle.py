@@ -57,6 +57,8 @@ def lib():
                                       C.POINTER(OrStats)]
         L.oracle_render.argtypes = [C.POINTER(OrScene), C.POINTER(OrFrame), C.c_int, C.c_int, P, P, C.c_int,
                                     C.c_int, C.c_int, C.POINTER(OrStats)]
+        L.oracle_render_rows.argtypes = [C.POINTER(OrScene), C.POINTER(OrFrame), C.c_int, C.c_int, P, P, P, C.c_int,
+                                         C.c_int, C.POINTER(OrStats)]
         L.oracle_trace_closest.argtypes = [C.POINTER(OrScene), C.c_uint32, P, C.c_int, P, P, P, C.POINTER(OrStats)]
         for fn in ("oracle_sin", "oracle_cos"):
             getattr(L, fn).argtypes = [C.c_float]
@@ -124,6 +126,14 @@ class Oracle:
         st = OrStats()
         lib().oracle_render(C.byref(self.scene), C.byref(f), frame_first, nframes, _p(accum), _p(out), y0,
                             f.height if y1 is None else y1, threads, C.byref(st))
+        return st.as_dict()
+
+    def render_rows(self, f: OrFrame, frame_first: int, nframes: int, accum: np.ndarray, out: np.ndarray, rows,
+                    threads=0) -> dict:
+        rows = np.ascontiguousarray(rows, np.int32)
+        st = OrStats()
+        lib().oracle_render_rows(C.byref(self.scene), C.byref(f), frame_first, nframes, _p(accum), _p(out), _p(rows),
+                                 len(rows), threads, C.byref(st))
         return st.as_dict()
 
     def trace_closest(self, bvh_count: int, rays: np.ndarray):

@@ -811,6 +811,37 @@ void oracle_render(const OrScene* s, const OrFrame* f, int frame_first, int nfra
   if (st) stats_add(st, &total);
 }
 
+void oracle_render_rows(const OrScene* s, const OrFrame* f, int frame_first, int nframes, float* accum,
+                        uint8_t* out, const int* rows, int nrows, int threads, OrStats* st) {
+  OrStats total; memset(&total, 0, sizeof total);
+#ifdef _OPENMP
+  if (threads <= 0) threads = omp_get_max_threads();
+  #pragma omp parallel num_threads(threads)
+  {
+    OrStats loc; memset(&loc, 0, sizeof loc);
+    #pragma omp for schedule(dynamic, 1)
+    for (int r = 0; r < nrows; ++r) {
+      for (int k = 0; k < nframes; ++k) {
+        OrFrame fk = *f; fk.accum_frames = frame_first + k; fk.reset = 0;
+        Cam cam = get_camera(&fk);
+        for (int x = 0; x < f->width; ++x) invocation(s, &fk, &cam, x, rows[r], accum, out, &loc);
+      }
+    }
+    #pragma omp critical
+    stats_add(&total, &loc);
+  }
+#else
+  (void)threads;
+  for (int r = 0; r < nrows; ++r)
+    for (int k = 0; k < nframes; ++k) {
+      OrFrame fk = *f; fk.accum_frames = frame_first + k; fk.reset = 0;
+      Cam cam = get_camera(&fk);
+      for (int x = 0; x < f->width; ++x) invocation(s, &fk, &cam, x, rows[r], accum, out, &total);
+    }
+#endif
+  if (st) stats_add(st, &total);
+}
+
 /* ray_intersects.glsl:135-161 (commented test kernel): per ray, hits = -1;
  * for each BVH: transform, Intersects(first_index, o', d', ray.t). */
 void oracle_trace_closest(const OrScene* s, uint32_t bvh_count, const OrRay* rays, int n, uint32_t* hits,

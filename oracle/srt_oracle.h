@@ -91,6 +91,10 @@ void oracle_dispatch(const OrScene* s, const OrFrame* f, float* accum, uint8_t* 
 void oracle_render(const OrScene* s, const OrFrame* f, int frame_first, int nframes,
                    float* accum, uint8_t* out, int y0, int y1, int threads, OrStats* st);
 
+/* As oracle_render over an explicit list of rows (bounded CPU-baseline samples). */
+void oracle_render_rows(const OrScene* s, const OrFrame* f, int frame_first, int nframes, float* accum,
+                        uint8_t* out, const int* rows, int nrows, int threads, OrStats* st);
+
 /* Closest-hit only: the (commented) test kernel ray_intersects.glsl:135-161. */
 void oracle_trace_closest(const OrScene* s, uint32_t bvh_count, const OrRay* rays, int n,
                           uint32_t* hits, float* t_out, float* n_out, OrStats* st);

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -60,8 +61,16 @@ struct KParams {
   int rank, nranks, band_rows, local_rows;
   int ext_w, ext_h;
   int stack_entries;
+  int nodes_f4, tris_f4;   // LDS-resident scene: sizes of the node / triangle arrays in float4
+  float4* lbuf;            // sample buffer: nframes x local_pixels radiance samples
+  int local_pixels;        // W * local_rows
+  int trav_frac16;         // resume shading when fewer than trav_frac16/16 of working lanes traverse
+  int stack_base_f4;       // first float4 of the per-lane stacks in dynamic LDS
   float cx, cy, cz, p00x, p00y, p00z, dux, duy, duz, dvx, dvy, dvz;
 };
+
+// Dynamic LDS of the path-tracing kernels: [scene copy (LDS mode)] [per-lane stacks].
+extern __shared__ __attribute__((aligned(16))) float4 g_smem[];
 
 enum { ST_RAYS = 0, ST_NODES, ST_TRIS, ST_RNGU, ST_RNGSQ, ST_LIGHTS, ST_MATS, ST_SAMPLES, ST_OVERFLOW, ST_MAXSTACK, ST_N };
 
@@ -117,19 +126,29 @@ struct Lane {
   int stride;
 };
 
+// (a % m) for 0 <= a, 0 < m, with the common case a < 2m handled by one compare
+__device__ __forceinline__ int wrap_index(int a, int m) {
+  if (a >= m) a -= m;
+  if (a >= m) a %= m;  // only when Width < Height (index base y*Height + x can exceed W*H)
+  return a;
+}
+
 // raytrace_utils.glsl:28-30
 __device__ __forceinline__ float rand_float(float sx, float sy) {
   const float d = sx * 12.9898f + sy * 78.233f;
   return fractf(sin_f(d) * 43758.5453f);
 }
 
-// raytrace_utils.glsl:44-54 randFloatSampleUniform
+// raytrace_utils.glsl:44-54 randFloatSampleUniform, split into the index and
+// the fetch so one bounce's independent draws are all in flight together.
+__device__ __forceinline__ int randU_index(const KParams& kp, const Lane& ln, float sx, float sy) {
+  const float r = rand_float(sx, sy) * (float)kp.W * (float)kp.H;
+  return wrap_index(ln.base + f2i(r), kp.WH);
+}
 template <bool COUNT>
 __device__ __forceinline__ float randU(const KParams& kp, const Lane& ln, Counters& c, float sx, float sy) {
-  const float r = rand_float(sx, sy) * (float)kp.W * (float)kp.H;
-  const int idx = (ln.base + f2i(r)) % kp.WH;
   bump<COUNT>(c, ST_RNGU);
-  return kp.noise_u[idx];
+  return kp.noise_u[randU_index(kp, ln, sx, sy)];
 }
 
 __device__ __forceinline__ float luminance(f3 c) { return c.x * 0.2126f + c.y * 0.7152f + c.z * 0.0722f; }
@@ -165,20 +184,29 @@ __device__ __forceinline__ uint32_t to_unorm8(float x) {
 // ---------------------------------------------------------------------------
 // BVH traversal (ray_intersects.glsl:49-133), order-exact
 // ---------------------------------------------------------------------------
+// IntersectsBox.  Hardware v_min/v_max (IEEE minNum/maxNum) give the same
+// value as GLSL min/max up to the sign of a zero result, and the result is
+// only ever compared (< dist, isinf), so every decision is unchanged.
 __device__ __forceinline__ float box_t(f3 o, f3 inv, float4 lo, float4 hi) {
   const float t0x = (lo.x - o.x) * inv.x, t0y = (lo.y - o.y) * inv.y, t0z = (lo.z - o.z) * inv.z;
   const float t1x = (hi.x - o.x) * inv.x, t1y = (hi.y - o.y) * inv.y, t1z = (hi.z - o.z) * inv.z;
-  const float tn = fmx(fmx(fmn(t0x, t1x), fmn(t0y, t1y)), fmn(t0z, t1z));
-  const float tf = fmn(fmn(fmx(t0x, t1x), fmx(t0y, t1y)), fmx(t0z, t1z));
+  const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t0x, t1x), __builtin_fminf(t0y, t1y)),
+                                   __builtin_fminf(t0z, t1z));
+  const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t0x, t1x), __builtin_fmaxf(t0y, t1y)),
+                                   __builtin_fmaxf(t0z, t1z));
   return tn <= tf ? ((tn >= 0.0f) ? tn : tf) : __builtin_inff();
 }
 
 __device__ __forceinline__ bool box_ok(float b, float dist) { return b < dist && !isinf_f(b); }
 
-// Moller-Trumbore with precomputed edges (ray_intersects.glsl:61-96)
-__device__ __forceinline__ bool tri_test(f3 o, f3 d, const float4* tp, float& dist) {
-  const float4 A = tp[0], B = tp[1], C = tp[2];
-  const f3 v0 = mk(A.x, A.y, A.z), e1 = mk(A.w, B.x, B.y), e2 = mk(B.z, B.w, C.x);
+// IntersectsTriangle (ray_intersects.glsl:61-96), Moller-Trumbore with edges
+// precomputed at upload.  The reference divides f = 1 / a per test; here an
+// approximate reciprocal (v_rcp_f32, 1 ulp) first REJECTS the triangles whose
+// u / v / u+v / t tests provably fail (margins of 2^-16 relative, far above the
+// <= 2^-21 combined rounding of the exact and approximate products); every
+// triangle not rejected that way is evaluated with the exact, correctly rounded
+// reference arithmetic, so the accept decision and t are bit-identical.
+__device__ __forceinline__ bool tri_test_exact(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& dist) {
   const f3 h = cross(d, e2);
   const float a = dot(e1, h);
   if (a > -0.0001f && a < 0.0001f) return false;
@@ -197,72 +225,161 @@ __device__ __forceinline__ bool tri_test(f3 o, f3 d, const float4* tp, float& di
   return false;
 }
 
+__device__ __forceinline__ bool tri_test(f3 o, f3 d, float4 A, float4 B, float4 C, float& dist) {
+  const f3 v0 = mk(A.x, A.y, A.z), e1 = mk(A.w, B.x, B.y), e2 = mk(B.z, B.w, C.x);
+  // every predicate below is evaluated without branching; only triangles
+  // that survive all conservative rejections take the exact path
+  const f3 h = cross(d, e2);
+  const float a = dot(e1, h);
+  const bool parallel = a > -0.0001f && a < 0.0001f;
+  const float r = __builtin_amdgcn_rcpf(a);
+  const f3 s = o - v0;
+  const float ua = r * dot(s, h);
+  const f3 q = cross(s, e1);
+  const float va = r * dot(d, q);
+  const float ta = r * dot(e2, q);
+  const bool in_range = __builtin_fabsf(a) < 1.0e30f;   // 1/a normal: the margins below hold
+  const bool reject = parallel |
+                      (in_range & ((ua < -1.0e-30f) | (ua > 1.0000153f) | (va < -1.0e-30f) |
+                                   (ua + va > 1.0f + 0.0000153f * __builtin_fmaxf(1.0f, va)) |
+                                   (ta < 0.0000099998f) | (ta > dist * 1.0000153f)));
+  if (reject) return false;
+  return tri_test_exact(o, d, v0, e1, e2, dist);
+}
+
+template <bool LDSM>
+__device__ __forceinline__ float4 node4(const KParams& kp, uint32_t i) {
+  if constexpr (LDSM) return g_smem[i];
+  else return kp.nodes[i];
+}
+template <bool LDSM>
+__device__ __forceinline__ float4 tri4(const KParams& kp, uint32_t i) {
+  if constexpr (LDSM) return g_smem[(uint32_t)kp.nodes_f4 + i];
+  else return kp.tris[i];
+}
+
+// Traversal stack entry: global mode 3 dwords (ref, count, t); LDS mode 2
+// dwords (ref | count << 24, t) -- LDS mode is only used for scenes whose
+// triangle / node indices fit 24 bits and leaves hold < 256 triangles.
+template <bool LDSM>
+__device__ __forceinline__ void stk_push(const Lane& ln, int sp, uint32_t ref, uint32_t cnt, float t) {
+  if constexpr (LDSM) {
+    ln.stk[(2 * sp + 0) * ln.stride] = ref | (cnt << 24);
+    ln.stk[(2 * sp + 1) * ln.stride] = __float_as_uint(t);
+  } else {
+    ln.stk[(3 * sp + 0) * ln.stride] = ref;
+    ln.stk[(3 * sp + 1) * ln.stride] = cnt;
+    ln.stk[(3 * sp + 2) * ln.stride] = __float_as_uint(t);
+  }
+}
+template <bool LDSM>
+__device__ __forceinline__ float stk_t(const Lane& ln, int sp) {
+  return __uint_as_float(ln.stk[((LDSM ? 2 : 3) * sp + (LDSM ? 1 : 2)) * ln.stride]);
+}
+template <bool LDSM>
+__device__ __forceinline__ void stk_ref(const Lane& ln, int sp, uint32_t& ref, uint32_t& cnt) {
+  if constexpr (LDSM) {
+    const uint32_t w = ln.stk[(2 * sp) * ln.stride];
+    ref = w & 0xFFFFFFu;
+    cnt = w >> 24;
+  } else {
+    ref = ln.stk[(3 * sp + 0) * ln.stride];
+    cnt = ln.stk[(3 * sp + 1) * ln.stride];
+  }
+}
+
 // Depth-first traversal in the reference's pop order (right child first).
 // Each child's box is tested once, when its parent is expanded; a child that
 // fails is never pushed (the running distance only shrinks, so it would fail
 // at its pop too); a pushed child is re-checked against the distance at pop
 // time with its stored entry distance (the same value IntersectsBox returns).
-template <bool ANY, bool COUNT>
+// `any`: stop at the first accepted triangle (shadow rays, CheckHit(...).hit).
+template <bool COUNT, bool LDSM>
 __device__ uint32_t traverse(const KParams& kp, const Lane& ln, Counters& c, uint32_t root, f3 o, f3 d,
-                             float& dist) {
+                             float& dist, bool any) {
+  // Flat loop: each iteration performs ONE step for the lane -- test one
+  // triangle of the current leaf, expand the current internal node, or pop --
+  // so lanes at leaves and lanes at internal nodes advance together.
+  // `ref`/`cnt` describe the current node as the reference's node record does
+  // (leaf: first triangle + remaining count; internal: index of its first
+  // child, cnt == 0); kNone = nothing current, pop next.
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
   const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-  uint32_t hit = 0xFFFFFFFFu;
-  const float4* N = kp.nodes;
-  float4 lo = N[2 * root + 2], hi = N[2 * root + 3];
+  uint32_t hit = kNone;
+  const float4 rlo = node4<LDSM>(kp, 2 * root + 2), rhi = node4<LDSM>(kp, 2 * root + 3);
   bump<COUNT>(c, ST_NODES);
-  if (!box_ok(box_t(o, inv, lo, hi), dist)) return hit;
-  uint32_t ref = __float_as_uint(lo.w), cnt = __float_as_uint(hi.w);
+  if (!box_ok(box_t(o, inv, rlo, rhi), dist)) return hit;
+  uint32_t ref = __float_as_uint(rlo.w), cnt = __float_as_uint(rhi.w);
   int sp = 0;
   for (;;) {
     if (cnt > 0) {
-      for (uint32_t i = 0; i < cnt; ++i) {
-        bump<COUNT>(c, ST_TRIS);
-        if (tri_test(o, d, kp.tris + 3 * (size_t)(ref + i), dist)) {
-          hit = ref + i;
-          if constexpr (ANY) return hit;
-        }
+      // leaf: one triangle per step, in the reference's order
+      bump<COUNT>(c, ST_TRIS);
+      const uint32_t t3 = 3 * ref;
+      if (tri_test(o, d, tri4<LDSM>(kp, t3), tri4<LDSM>(kp, t3 + 1), tri4<LDSM>(kp, t3 + 2), dist)) {
+        hit = ref;
+        if (any) break;
       }
-    } else {
-      const float4* P = N + 2 * (size_t)ref + 2;
-      const float4 l0 = P[0], h0 = P[1], l1 = P[2], h1 = P[3];
+      ++ref;
+      if (--cnt == 0) ref = kNone;
+    } else if (ref != kNone) {
+      // internal: test both children now.  The reference pushes c0 then c1
+      // and pops c1 first; a child whose box fails is never needed (the
+      // distance only shrinks), a lone passing child is visited directly.
+      const uint32_t pi = 2 * ref + 2;
+      const float4 l0 = node4<LDSM>(kp, pi), h0 = node4<LDSM>(kp, pi + 1);
+      const float4 l1 = node4<LDSM>(kp, pi + 2), h1 = node4<LDSM>(kp, pi + 3);
       bump<COUNT>(c, ST_NODES, 2);
       const float b0 = box_t(o, inv, l0, h0);
       const float b1 = box_t(o, inv, l1, h1);
       const bool v0 = box_ok(b0, dist), v1 = box_ok(b1, dist);
-      if (v0) {
+      const uint32_t r0 = __float_as_uint(l0.w), n0 = __float_as_uint(h0.w);
+      if (v0 & v1) {
         if (sp >= kp.stack_entries) {  // cannot happen for a validated BVH
           bump<COUNT>(c, ST_OVERFLOW);
-          return hit;
+          break;
         }
-        ln.stk[(3 * sp + 0) * ln.stride] = __float_as_uint(l0.w);
-        ln.stk[(3 * sp + 1) * ln.stride] = __float_as_uint(h0.w);
-        ln.stk[(3 * sp + 2) * ln.stride] = __float_as_uint(b0);
+        stk_push<LDSM>(ln, sp, r0, n0, b0);
         ++sp;
         if constexpr (COUNT) {
-          if ((uint32_t)sp + 1 > c.v[ST_MAXSTACK]) c.v[ST_MAXSTACK] = (uint32_t)sp + 1;
+          if ((uint32_t)sp > c.v[ST_MAXSTACK]) c.v[ST_MAXSTACK] = (uint32_t)sp;
         }
       }
-      if (v1) {
-        ref = __float_as_uint(l1.w);
-        cnt = __float_as_uint(h1.w);
-        continue;
-      }
+      ref = v1 ? __float_as_uint(l1.w) : (v0 ? r0 : kNone);
+      cnt = v1 ? __float_as_uint(h1.w) : (v0 ? n0 : 0u);
     }
-    // pop the next entry that still beats the running distance
-    bool found = false;
-    while (sp > 0) {
+    if (cnt == 0 && ref == kNone) {
+      // pop one entry; it is visited if it still beats the running distance
+      if (sp == 0) break;
       --sp;
-      const float bt = __uint_as_float(ln.stk[(3 * sp + 2) * ln.stride]);
-      if (bt < dist) {
-        ref = ln.stk[(3 * sp + 0) * ln.stride];
-        cnt = ln.stk[(3 * sp + 1) * ln.stride];
-        found = true;
-        break;
-      }
+      if (stk_t<LDSM>(ln, sp) < dist) stk_ref<LDSM>(ln, sp, ref, cnt);
     }
-    if (!found) break;
   }
   return hit;
+}
+
+__device__ __forceinline__ f3 xform(const float* m, f3 v, float w) {
+  return mk(((m[0] * v.x + m[4] * v.y) + m[8] * v.z) + m[12] * w,
+            ((m[1] * v.x + m[5] * v.y) + m[9] * v.z) + m[13] * w,
+            ((m[2] * v.x + m[6] * v.y) + m[10] * v.z) + m[14] * w);
+}
+
+// CheckHit over the model BVHs (raytrace_compute.glsl:143-162): closest hit
+// triangle (dist updated), or with `any` the first accepted triangle.
+template <bool COUNT, bool LDSM>
+__device__ uint32_t trace_mesh(const KParams& kp, const Lane& ln, Counters& c, f3 ro, f3 rd, float& dist, bool any) {
+  uint32_t hit_tri = 0xFFFFFFFFu;
+  for (uint32_t i = 0; i < kp.bvh_count; ++i) {
+    const srt_bvh_record& b = kp.bvhs[i];
+    const f3 to = xform(b.frame, ro, 1.0f);
+    const f3 td = xform(b.frame, rd, 0.0f);
+    const uint32_t h = traverse<COUNT, LDSM>(kp, ln, c, b.first_index, to, td, dist, any);
+    if (h != 0xFFFFFFFFu) {
+      hit_tri = h;
+      if (any) break;
+    }
+  }
+  return hit_tri;
 }
 
 // raytrace_compute.glsl:93-120 SphereHit
@@ -285,93 +402,21 @@ __device__ __forceinline__ bool sphere_hit(f3 ro, f3 rd, f3 pos, float radius, f
   return true;
 }
 
-__device__ __forceinline__ f3 xform(const float* m, f3 v, float w) {
-  return mk(((m[0] * v.x + m[4] * v.y) + m[8] * v.z) + m[12] * w,
-            ((m[1] * v.x + m[5] * v.y) + m[9] * v.z) + m[13] * w,
-            ((m[2] * v.x + m[6] * v.y) + m[10] * v.z) + m[14] * w);
-}
-
-// raytrace_compute.glsl:122-165 CheckHit (closest hit, full record)
-template <bool COUNT>
-__device__ Hit check_hit(const KParams& kp, const Lane& ln, Counters& c, f3 ro, f3 rd, float mn, float mx) {
-  Hit rec;
-  rec.hit = false;
-  bump<COUNT>(c, ST_RAYS);
-  float dist = mx;
-  if (!kp.show_model) {
-    int best = -1;
-    f3 best_p = mk(0.f, 0.f, 0.f);
-    float best_t = 0.f;
-    for (int i = 0; i < 5; ++i) {
-      f3 pos; float radius; Mat m;
-      sphere_data(i, pos, radius, m);
-      float t;
-      if (sphere_hit(ro, rd, pos, radius, mn, dist, t)) {
-        best = i;
-        best_t = t;
-        dist = t;
-      }
-    }
-    if (best >= 0) {
-      f3 pos; float radius; Mat m;
-      sphere_data(best, pos, radius, m);
-      rec.hit = true;
-      best_p = ro + rd * best_t;
-      rec.p = best_p;
-      rec.mat = m;
-      const f3 outward = (best_p - pos) / radius;   // SetFaceNormal (raytrace_utils.glsl:23-26)
-      rec.normal = (dot(rd, outward) < 0.0f) ? outward : -outward;
-    }
-  } else {
-    uint32_t hit_tri = 0xFFFFFFFFu;
-    for (uint32_t i = 0; i < kp.bvh_count; ++i) {
-      const srt_bvh_record& b = kp.bvhs[i];
-      const f3 to = xform(b.frame, ro, 1.0f);
-      const f3 td = xform(b.frame, rd, 0.0f);
-      const uint32_t h = traverse<false, COUNT>(kp, ln, c, b.first_index, to, td, dist);
-      if (h != 0xFFFFFFFFu) hit_tri = h;
-    }
-    if (hit_tri != 0xFFFFFFFFu) {
-      rec.hit = true;
-      rec.p = (dist * rd) + ro;
-      const float4* tp = kp.tris + 3 * (size_t)hit_tri;
-      const float4 A = tp[0], B = tp[1], C = tp[2];
-      const f3 e1 = mk(A.w, B.x, B.y), e2 = mk(B.z, B.w, C.x);
-      rec.normal = normalize(cross(e1, e2));
-      const uint32_t mi = __float_as_uint(C.y);
-      const float4 m0 = kp.mats[2 * mi], m1 = kp.mats[2 * mi + 1];
-      bump<COUNT>(c, ST_MATS);
-      rec.mat.albedo = mk(m0.x, m0.y, m0.z);
-      rec.mat.roughness = m0.w;
-      rec.mat.specular = mk(m1.x, m1.y, m1.z);
-      rec.mat.metalness = 0.1f;
-      rec.mat.useSpec = true;
+// CheckHit over the five spheres (raytrace_compute.glsl:132-141): index of the
+// closest sphere (dist updated) or, with `any`, of the first sphere hit; -1 if none.
+__device__ __forceinline__ int trace_spheres(f3 ro, f3 rd, float mn, float& dist, bool any) {
+  int best = -1;
+  for (int i = 0; i < 5; ++i) {
+    f3 pos; float radius; Mat m;
+    sphere_data(i, pos, radius, m);
+    float t;
+    if (sphere_hit(ro, rd, pos, radius, mn, dist, t)) {
+      best = i;
+      dist = t;
+      if (any) break;
     }
   }
-  return rec;
-}
-
-// CheckHit(...).hit for the shadow ray of CheckLightOccluded (raytrace_compute.glsl:167-176)
-template <bool COUNT>
-__device__ bool any_hit(const KParams& kp, const Lane& ln, Counters& c, f3 ro, f3 rd, float mn, float mx) {
-  bump<COUNT>(c, ST_RAYS);
-  if (!kp.show_model) {
-    for (int i = 0; i < 5; ++i) {
-      f3 pos; float radius; Mat m;
-      sphere_data(i, pos, radius, m);
-      float t;
-      if (sphere_hit(ro, rd, pos, radius, mn, mx, t)) return true;
-    }
-    return false;
-  }
-  for (uint32_t i = 0; i < kp.bvh_count; ++i) {
-    const srt_bvh_record& b = kp.bvhs[i];
-    const f3 to = xform(b.frame, ro, 1.0f);
-    const f3 td = xform(b.frame, rd, 0.0f);
-    float dist = mx;
-    if (traverse<true, COUNT>(kp, ln, c, b.first_index, to, td, dist) != 0xFFFFFFFFu) return true;
-  }
-  return false;
+  return best;
 }
 
 __device__ __forceinline__ float light_falloff(f3 p, const LightRec& L) {
@@ -390,37 +435,6 @@ __device__ __forceinline__ LightRec load_light(const KParams& kp, Counters& c, i
   const int i = (idx >= 0 && idx < kp.light_records) ? idx : kp.light_records;  // zero record
   const float4 a = kp.lights[2 * i], b = kp.lights[2 * i + 1];
   return LightRec{mk(a.x, a.y, a.z), a.w, mk(b.x, b.y, b.z)};
-}
-
-// raytrace_compute.glsl:179-206 SampleLights.  randLightIndex uses the same
-// seed every iteration, so the light (and its pdf) is loop-invariant; once a
-// light is selected later iterations only re-select it, so their random
-// draws are skipped (the result is unchanged).
-template <bool COUNT>
-__device__ bool sample_lights(const KParams& kp, const Lane& ln, Counters& c, f3 p, float& weight, LightRec& sel) {
-  const int n = kp.light_count;
-  float total = 0.0f, pdf = 0.0f;
-  bool selected = false;
-  if (n > 0) {
-    const int idx = f2i(__builtin_rintf(randU<COUNT>(kp, ln, c, p.x, p.y) * (float)n));
-    sel = load_light<COUNT>(kp, c, idx);
-    const float fo = light_falloff(p, sel);
-    const float inten = sel.intensity * fo;
-    const float lpdf = luminance(mk(inten, inten, inten));
-    const float ris = lpdf * (float)n;
-    for (int i = 0; i < n; ++i) {
-      total += ris;
-      if (!selected) {
-        const float r = randU<COUNT>(kp, ln, c, p.y + (float)i, p.z + (float)i);
-        if (r < (ris / total)) {
-          pdf = lpdf;
-          selected = true;
-        }
-      }
-    }
-  }
-  weight = (total / (float)n) / fmx(0.001f, pdf);
-  return selected;
 }
 
 __device__ __forceinline__ float ggxD(float NdotH, float rough) {
@@ -450,8 +464,9 @@ __device__ __forceinline__ float smithG2(float alpha, float NdotL, float NdotV) 
   return 1.0f / (1.0f + smithLambda(aL) + smithLambda(aV));
 }
 
-// brdf.glsl:200-224 SampleDirect
-__device__ f3 sample_direct(const Hit& hit, f3 Vv, const LightRec& L, float shadow) {
+// brdf.glsl:200-224 SampleDirect up to the shadow factor: returns
+// (ggxTerm + NdotL * albedo / pi) and the light term's unshadowed factors.
+__device__ f3 sample_direct_brdf(const Hit& hit, f3 Vv, const LightRec& L, float& li) {
   const f3 Ld = light_dir(L, hit.p);
   const f3 vl = Vv + Ld;
   const f3 H = length(vl) > 0.0f ? normalize(vl) : vl;
@@ -465,11 +480,10 @@ __device__ f3 sample_direct(const Hit& hit, f3 Vv, const LightRec& L, float shad
   const float G = ggxSchlickMasking(NdotL, NdotV, rough);
   const f3 F = schlickFresnel(hit.mat.specular, LdotH);
   const float fo = light_falloff(hit.p, L);
-  const float li = L.intensity * fo;
+  li = L.intensity * fo;
   const f3 ggx = (F * (D * G)) / (4.0f * fmx(0.001f, NdotV));
-  const f3 lt = (shadow * L.color) * li;
   const f3 diff = (NdotL * hit.mat.albedo) / 3.1415926535897f;
-  return lt * (ggx + diff);
+  return ggx + diff;
 }
 
 // brdf.glsl:226-237 SampleDirectNew (GetAllBRDFValues :173-198, EvalSpecular :139-145
@@ -522,18 +536,15 @@ __device__ __forceinline__ f3 reflect3(f3 I, f3 N) { return I - N * (2.0f * dot(
 #define DIFFUSE_BRDF 1
 #define SPECULAR_BRDF 2
 
-// brdf.glsl:239-277 SampleIndirectNew.  SampleDiffuse (:60-74) and
-// SampleSpecularHalfVec (:81-99) draw the same two numbers (seeds p.xy, p.yz).
-template <bool COUNT>
-__device__ bool sample_indirect(const KParams& kp, const Lane& ln, Counters& c, const Hit& hit, f3 Vv, int type,
-                                f3& dir, f3& weight) {
+// brdf.glsl:239-277 SampleIndirectNew with its uniform draws r1 = U(p.xy),
+// r2 = U(p.yz) supplied (SampleDiffuse :60-74 and SampleSpecularHalfVec :81-99
+// both draw exactly these two numbers).
+__device__ bool sample_indirect(const Hit& hit, f3 Vv, int type, float r1, float r2, f3& dir, f3& weight) {
   const f3 N = hit.normal;
   if (dot(N, Vv) <= 0.0f) return false;
   const f3 specF0 = specularF0(hit.mat.albedo, hit.mat.metalness);
   f3 nd;
   if (type == DIFFUSE_BRDF) {
-    const float r1 = randU<COUNT>(kp, ln, c, hit.p.x, hit.p.y);
-    const float r2 = randU<COUNT>(kp, ln, c, hit.p.y, hit.p.z);
     const f3 B = perpendicular(N);
     const f3 T = cross(B, N);
     const float r = __builtin_sqrtf(__builtin_fabsf(r1));
@@ -552,9 +563,7 @@ __device__ bool sample_indirect(const KParams& kp, const Lane& ln, Counters& c, 
       const f3 Lt = reflect3(-Vv, N);
       H = normalize(-Vv + Lt);
     } else {
-      const float rx = randU<COUNT>(kp, ln, c, hit.p.x, hit.p.y);
-      const float ry = randU<COUNT>(kp, ln, c, hit.p.y, hit.p.z);
-      H = specular_half(rx, ry, hit.mat.roughness, N);
+      H = specular_half(r1, r2, hit.mat.roughness, N);
     }
     const f3 L = reflect3(-Vv, H);
     const float HdotL = fmx(0.00001f, fmn(1.0f, dot(H, L)));
@@ -568,65 +577,6 @@ __device__ bool sample_indirect(const KParams& kp, const Lane& ln, Counters& c, 
   dir = normalize(nd);
   if (dot(N, dir) <= 0.0f) return false;
   return true;
-}
-
-// raytrace_compute.glsl:208-294 GetRayColor
-template <bool COUNT>
-__device__ f3 ray_color(const KParams& kp, const Lane& ln, Counters& c, f3 ro, f3 rd) {
-  int randIndex = 0;
-  int depth = kp.max_depth;
-  f3 T = mk(1.0f, 1.0f, 1.0f);
-  f3 color = mk(0.0f, 0.0f, 0.0f);
-  for (;;) {
-    const Hit rec = check_hit<COUNT>(kp, ln, c, ro, rd, 0.001f, __builtin_inff());
-    if (!rec.hit) break;
-    float lw;
-    LightRec L;
-    const bool sampled = sample_lights<COUNT>(kp, ln, c, rec.p, lw, L);
-    const f3 Vv = -rd;
-    if (sampled) {
-      const f3 toL = L.pos - rec.p;
-      const f3 sdir = normalize(toL);
-      const float smax = length(toL);
-      const float shadow = any_hit<COUNT>(kp, ln, c, rec.p, sdir, 0.001f, smax) ? 0.0f : 1.0f;
-      if (rec.mat.useSpec) {
-        color = color + (T * sample_direct(rec, Vv, L, shadow)) * lw;
-      } else {
-        const f3 Ld = light_dir(L, rec.p);
-        const float fo = light_falloff(rec.p, L);
-        const f3 li = ((L.color * fo) * L.intensity) * lw;
-        color = color + ((T * sample_direct_new(rec, Vv, Ld)) * shadow) * li;
-      }
-    }
-    int type;
-    if (rec.mat.metalness == 1.0f && rec.mat.roughness == 0.0f) {
-      type = SPECULAR_BRDF;
-    } else {
-      const float bp = brdf_probability(rec.mat, Vv, rec.normal);
-      const float r = randU<COUNT>(kp, ln, c, rec.p.x + (float)depth, rec.p.y + (float)depth);
-      if (r < bp) {
-        type = SPECULAR_BRDF;
-        T = T / bp;
-      } else {
-        type = DIFFUSE_BRDF;
-        T = T / (1.0f - bp);
-      }
-    }
-    if (depth <= 0) {
-      const float surv = clampf(luminance(T), 0.1f, 1.0f);
-      if (randU<COUNT>(kp, ln, c, rec.p.x + (float)randIndex, rec.p.y + (float)randIndex) > surv) break;
-      T = T / surv;
-      randIndex++;
-    } else {
-      depth--;
-    }
-    f3 dir, bw;
-    if (!sample_indirect<COUNT>(kp, ln, c, rec, Vv, type, dir, bw)) break;
-    T = T * bw;
-    rd = dir;
-    ro = rec.p;
-  }
-  return color + T * mk(0.05f, 0.05f, 0.05f);
 }
 
 template <bool COUNT>
@@ -643,68 +593,448 @@ __device__ __forceinline__ void flush_counters(const KParams& kp, const Counters
 }
 
 // ---------------------------------------------------------------------------
-// kernels
+// the path-tracing kernels
 // ---------------------------------------------------------------------------
-// Pixel mapping: a 256-thread block covers 16x16 local pixels as four 8x8
-// wave tiles (the reference's local_size 8x8, raytrace_compute.glsl:12).
-template <bool COUNT>
-__global__ __launch_bounds__(256) void pathtrace_kernel(KParams kp) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63;
-  const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-  const int ly = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-  if (x >= kp.ext_w || ly >= kp.local_rows) return;
-  const int band = ly / kp.band_rows;
-  const int gy = (band * kp.nranks + kp.rank) * kp.band_rows + (ly - band * kp.band_rows);
-  if (gy >= kp.ext_h) return;
-  const size_t li = (size_t)ly * (size_t)kp.W + (size_t)x;
-  if (kp.reset) {  // raytrace_compute.glsl:390-393
-    kp.accum[li] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-    return;
+// Work decomposition.  The reference accumulates one path sample per pixel
+// per frame: accum = (((accum + L_f0) + L_f0+1) + ...) (raytrace_compute.glsl:
+// 400-406).  Every sample L_k is independent (all randomness is a pure
+// function of pixel, frame and hit position), only the SUM is ordered.  So
+//   sample_kernel     computes samples (pixel, frame) in any order on any lane
+//                     and stores each L_k (16 B) to an HBM sample buffer;
+//   accumulate_kernel adds them per pixel in frame order (bit-identical sum)
+//                     and writes the sRGB8 image.
+// sample_kernel is persistent: each wave walks its own round-robin share of
+// 64-item batches (an 8x8 tile of one frame); lanes whose path has ended take
+// the next items of the wave's batch with a ballot + prefix count, so lanes
+// stay busy regardless of per-pixel path cost.  Traversal is resumable: a
+// wave steps all traversing lanes until fewer than a threshold remain, then
+// shades the lanes whose ray has returned (and refills them) while the rest
+// keep their traversal state (registers + LDS stack) for the next round.
+// ---------------------------------------------------------------------------
+struct Trav {
+  f3 o, d, inv;       // ray in the current BVH's frame
+  float dist;         // running intersection_distance
+  uint32_t ref, cnt;  // current node (leaf: first triangle + remaining; internal: first child)
+  uint32_t hit;       // best triangle so far (0xFFFFFFFF: none)
+  uint32_t bi;        // current BVH
+  int sp;
+  bool active;        // still traversing
+  bool start;         // next step sets up BVH `bi`
+};
+
+constexpr uint32_t kNoneRef = 0xFFFFFFFFu;
+
+// One traversal step (see traverse() for the order argument).  `ro`/`rd` are
+// the world-space ray, `any` selects the shadow-ray (first hit) variant.
+template <bool COUNT, bool LDSM>
+__device__ __forceinline__ void trav_step(const KParams& kp, const Lane& ln, Counters& c, Trav& t, f3 ro, f3 rd,
+                                          bool any) {
+  if (t.start) {
+    const srt_bvh_record& b = kp.bvhs[t.bi];
+    t.o = xform(b.frame, ro, 1.0f);
+    t.d = xform(b.frame, rd, 0.0f);
+    t.inv = mk(1.0f / t.d.x, 1.0f / t.d.y, 1.0f / t.d.z);
+    const uint32_t root = b.first_index;
+    const float4 rlo = node4<LDSM>(kp, 2 * root + 2), rhi = node4<LDSM>(kp, 2 * root + 3);
+    bump<COUNT>(c, ST_NODES);
+    const bool ok = box_ok(box_t(t.o, t.inv, rlo, rhi), t.dist);
+    t.ref = ok ? __float_as_uint(rlo.w) : kNoneRef;
+    t.cnt = ok ? __float_as_uint(rhi.w) : 0u;
+    t.sp = 0;
+    t.start = false;
+  } else if (t.cnt > 0) {
+    bump<COUNT>(c, ST_TRIS);
+    const uint32_t t3 = 3 * t.ref;
+    if (tri_test(t.o, t.d, tri4<LDSM>(kp, t3), tri4<LDSM>(kp, t3 + 1), tri4<LDSM>(kp, t3 + 2), t.dist)) {
+      t.hit = t.ref;
+      if (any) {
+        t.active = false;
+        return;
+      }
+    }
+    ++t.ref;
+    if (--t.cnt == 0) t.ref = kNoneRef;
+  } else if (t.ref != kNoneRef) {
+    const uint32_t pi = 2 * t.ref + 2;
+    const float4 l0 = node4<LDSM>(kp, pi), h0 = node4<LDSM>(kp, pi + 1);
+    const float4 l1 = node4<LDSM>(kp, pi + 2), h1 = node4<LDSM>(kp, pi + 3);
+    bump<COUNT>(c, ST_NODES, 2);
+    const float b0 = box_t(t.o, t.inv, l0, h0);
+    const float b1 = box_t(t.o, t.inv, l1, h1);
+    const bool v0 = box_ok(b0, t.dist), v1 = box_ok(b1, t.dist);
+    const uint32_t r0 = __float_as_uint(l0.w), n0 = __float_as_uint(h0.w);
+    if (v0 & v1) {
+      if (t.sp >= kp.stack_entries) {  // cannot happen for a validated BVH
+        bump<COUNT>(c, ST_OVERFLOW);
+        t.active = false;
+        return;
+      }
+      stk_push<LDSM>(ln, t.sp, r0, n0, b0);
+      ++t.sp;
+      if constexpr (COUNT) {
+        if ((uint32_t)t.sp > c.v[ST_MAXSTACK]) c.v[ST_MAXSTACK] = (uint32_t)t.sp;
+      }
+    }
+    t.ref = v1 ? __float_as_uint(l1.w) : (v0 ? r0 : kNoneRef);
+    t.cnt = v1 ? __float_as_uint(h1.w) : (v0 ? n0 : 0u);
   }
+  if (t.cnt == 0 && t.ref == kNoneRef) {
+    if (t.sp > 0) {
+      --t.sp;
+      if (stk_t<LDSM>(ln, t.sp) < t.dist) stk_ref<LDSM>(ln, t.sp, t.ref, t.cnt);
+    } else if ((any && t.hit != kNoneRef) || t.bi + 1 >= kp.bvh_count) {
+      t.active = false;  // CheckHit's loop over bvh_count is complete
+    } else {
+      ++t.bi;
+      t.start = true;
+    }
+  }
+}
+
+__device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
+  return __popcll(mask & ((1ull << lane) - 1ull));
+}
+
+template <bool COUNT, bool LDSM>
+__global__ __launch_bounds__(LDSM ? 1024 : 256) void sample_kernel(KParams kp) {
+  const int tid = threadIdx.x;
+  if constexpr (LDSM) {  // the block copies the scene (nodes + triangles) into LDS once
+    const int total = kp.nodes_f4 + kp.tris_f4;
+    for (int i = tid; i < total; i += blockDim.x)
+      g_smem[i] = (i < kp.nodes_f4) ? kp.nodes[i] : kp.tris[i - kp.nodes_f4];
+    __syncthreads();
+  }
+  const int lane = tid & 63;
+  const int n_waves = (int)(gridDim.x * (blockDim.x >> 6));
+  const int wave_id = (int)(blockIdx.x * (blockDim.x >> 6)) + (tid >> 6);
   Lane ln;
-  ln.base = gy * kp.H + x;
-  ln.stk = lds + tid;
+  ln.stk = reinterpret_cast<uint32_t*>(g_smem + kp.stack_base_f4) + tid;
   ln.stride = blockDim.x;
+  ln.base = 0;
   Counters c;
   for (int k = 0; k < ST_N; ++k) c.v[k] = 0;
+
   const f3 center = mk(kp.cx, kp.cy, kp.cz);
-  const f3 p00 = mk(kp.p00x, kp.p00y, kp.p00z);
-  const f3 du = mk(kp.dux, kp.duy, kp.duz);
-  const f3 dv = mk(kp.dvx, kp.dvy, kp.dvz);
+  const int tiles_x = (kp.W + 7) >> 3;
+  const int n_tiles = tiles_x * ((kp.local_rows + 7) >> 3);
+  const long long n_batches = (long long)n_tiles * kp.nframes;
+  long long batch = wave_id;  // this wave's batches: wave_id, wave_id + n_waves, ...
+  int batch_next = 0;         // items of `batch` already handed out
+
+  // per-lane sample / path / traversal state
+  bool has_work = false;
+  int x = 0, gy = 0, li = 0, fidx = 0;
+  f3 ro = mk(0.f, 0.f, 0.f), rd = mk(0.f, 0.f, 1.f), T, color, q0, q1, nd;
+  float tmax = 0.0f;
+  int depth = 0, randIndex = 0, hit_sphere = -1, bounces = 0;
+  bool shadow_phase = false, term = false;
+  Trav tr;
+  tr.active = false;
+  tr.start = false;
+  tr.hit = kNoneRef;
+
+  auto start_ray = [&]() {
+    tr.dist = tmax;
+    tr.hit = kNoneRef;
+    tr.bi = 0;
+    tr.active = true;
+    tr.start = true;
+    bump<COUNT>(c, ST_RAYS);
+    if (!kp.show_model) {  // the five spheres are "traversed" in one go
+      float dist = tmax;
+      hit_sphere = trace_spheres(ro, rd, 0.001f, dist, shadow_phase);
+      tr.dist = dist;
+      tr.active = false;
+    }
+  };
+  auto finish_sample = [&]() {
+    color = color + T * mk(0.05f, 0.05f, 0.05f);  // skyColor, raytrace_compute.glsl:219,292
+    kp.lbuf[(size_t)fidx * (size_t)kp.local_pixels + (size_t)li] = make_float4(color.x, color.y, color.z, 0.0f);
+    has_work = false;
+  };
+
+  for (;;) {
+    // ---- (A) idle lanes take the next items of the wave's batches ----
+    for (;;) {
+      const unsigned long long idle = __ballot(!has_work);
+      if (idle == 0ull || batch >= n_batches) break;
+      const int avail = 64 - batch_next;
+      const int r = lane_rank(idle, lane);
+      if (!has_work && r < avail) {
+        const int item = batch_next + r;
+        const int tile = (int)(batch % n_tiles);
+        const int frame_i = (int)(batch / n_tiles);
+        const int tx = tile % tiles_x, ty = tile / tiles_x;
+        const int px = tx * 8 + (item & 7), ly = ty * 8 + (item >> 3);
+        if (px < kp.ext_w && ly < kp.local_rows) {
+          const int band = ly / kp.band_rows;
+          const int yy = (band * kp.nranks + kp.rank) * kp.band_rows + (ly - band * kp.band_rows);
+          if (yy < kp.ext_h) {
+            has_work = true;
+            x = px;
+            gy = yy;
+            li = ly * kp.W + px;
+            fidx = frame_i;
+            ln.base = gy * kp.H + x;
+            // GetRay (raytrace_compute.glsl:78-90) with SampleSquare (raytrace_utils.glsl:10-17)
+            const int samp = (kp.frame_first + frame_i) % kp.WH;
+            const float2 nz = kp.noise_xy[wrap_index(ln.base + samp, kp.WH)];
+            bump<COUNT>(c, ST_RNGSQ);
+            bump<COUNT>(c, ST_SAMPLES);
+            const f3 p00 = mk(kp.p00x, kp.p00y, kp.p00z);
+            const f3 du = mk(kp.dux, kp.duy, kp.duz);
+            const f3 dv = mk(kp.dvx, kp.dvy, kp.dvz);
+            const f3 ps = (p00 + du * ((float)x + (nz.x - 0.5f))) + dv * ((float)gy + (nz.y - 0.5f));
+            ro = center;
+            rd = ps - center;
+            tmax = __builtin_inff();
+            T = mk(1.0f, 1.0f, 1.0f);
+            color = mk(0.0f, 0.0f, 0.0f);
+            depth = kp.max_depth;
+            randIndex = 0;
+            bounces = 0;
+            shadow_phase = false;
+            term = false;
+            start_ray();
+          }
+        }
+      }
+      const int taken = __popcll(idle) < avail ? __popcll(idle) : avail;
+      batch_next += taken;
+      if (batch_next == 64) {
+        batch += n_waves;
+        batch_next = 0;
+      }
+    }
+    if (__ballot(has_work) == 0ull) break;
+
+    // ---- (B) traverse until too few lanes are still traversing ----
+    if (kp.show_model) {
+      for (;;) {
+        const unsigned long long trav = __ballot(tr.active);
+        if (trav == 0ull) break;
+        const int n_trav = __popcll(trav);
+        const int n_work = __popcll(__ballot(has_work));
+        if (n_trav < n_work && n_trav * 16 < n_work * kp.trav_frac16) break;
+        if (tr.active) trav_step<COUNT, LDSM>(kp, ln, c, tr, ro, rd, shadow_phase);
+      }
+    }
+
+    // ---- (C) lanes whose ray returned: shade (GetRayColor's loop body) ----
+    if (has_work && !tr.active) {
+      const bool hit = kp.show_model ? (tr.hit != kNoneRef) : (hit_sphere >= 0);
+      const float dist = tr.dist;
+      if (shadow_phase) {  // CheckLightOccluded returned: this bounce's direct light
+        color = color + (hit ? q0 : q1);
+        if (term) {
+          finish_sample();
+        } else {
+          rd = nd;  // the bounce ray starts at the same hit point as the shadow ray
+          tmax = __builtin_inff();
+          shadow_phase = false;
+          start_ray();
+        }
+      } else if (!hit) {
+        finish_sample();
+      } else {
+        // ---- hit record (CheckHit) ----
+        Hit rec;
+        rec.hit = true;
+        if (kp.show_model) {
+          rec.p = (dist * rd) + ro;
+          const uint32_t ht = tr.hit;
+          const float4 A = tri4<LDSM>(kp, 3 * ht), B = tri4<LDSM>(kp, 3 * ht + 1), C = tri4<LDSM>(kp, 3 * ht + 2);
+          rec.normal = normalize(cross(mk(A.w, B.x, B.y), mk(B.z, B.w, C.x)));
+          const uint32_t mi = __float_as_uint(C.y);
+          const float4 m0 = kp.mats[2 * mi], m1 = kp.mats[2 * mi + 1];
+          bump<COUNT>(c, ST_MATS);
+          rec.mat.albedo = mk(m0.x, m0.y, m0.z);
+          rec.mat.roughness = m0.w;
+          rec.mat.specular = mk(m1.x, m1.y, m1.z);
+          rec.mat.metalness = 0.1f;
+          rec.mat.useSpec = true;
+        } else {
+          f3 pos; float radius;
+          sphere_data(hit_sphere, pos, radius, rec.mat);
+          rec.p = ro + rd * dist;
+          const f3 outward = (rec.p - pos) / radius;   // SetFaceNormal (raytrace_utils.glsl:23-26)
+          rec.normal = (dot(rd, outward) < 0.0f) ? outward : -outward;
+        }
+        const f3 p = rec.p;
+        const f3 Vv = -rd;
+
+        // ---- this bounce's independent uniform draws, fetched together ----
+        const int n = kp.light_count;
+        const bool fixed_spec = (rec.mat.metalness == 1.0f && rec.mat.roughness == 0.0f);
+        const int i_r1 = randU_index(kp, ln, p.x, p.y);             // light index; SampleDiffuse r1
+        const int i_r2 = randU_index(kp, ln, p.y, p.z);             // SampleDiffuse r2
+        const int i_sel = randU_index(kp, ln, p.y + 0.0f, p.z + 0.0f);
+        const int i_bp = randU_index(kp, ln, p.x + (float)depth, p.y + (float)depth);
+        const bool rr = depth <= 0;
+        const int i_rr = rr ? randU_index(kp, ln, p.x + (float)randIndex, p.y + (float)randIndex) : 0;
+        const float r1 = kp.noise_u[i_r1];
+        const float r2 = kp.noise_u[i_r2];
+        const float u_sel0 = kp.noise_u[i_sel];
+        const float u_bp = kp.noise_u[i_bp];
+        const float u_rr = rr ? kp.noise_u[i_rr] : 1.0f;
+        if constexpr (COUNT) c.v[ST_RNGU] += 4 + (rr ? 1 : 0);
+
+        // ---- SampleLights (raytrace_compute.glsl:179-206) ----
+        // randLightIndex uses the same seed every iteration, so the light and its
+        // pdf are loop-invariant; after the first selection later iterations only
+        // re-select it, so their draws are skipped (the result is unchanged).
+        bool selected = false;
+        float lw = 0.0f;
+        LightRec L;
+        if (n > 0) {
+          L = load_light<COUNT>(kp, c, f2i(__builtin_rintf(r1 * (float)n)));
+          const float fo = light_falloff(p, L);
+          const float inten = L.intensity * fo;
+          const float lpdf = luminance(mk(inten, inten, inten));
+          const float ris = lpdf * (float)n;
+          float total = 0.0f, pdf = 0.0f;
+          for (int i = 0; i < n; ++i) {
+            total += ris;
+            if (!selected) {
+              const float r = (i == 0) ? u_sel0 : randU<COUNT>(kp, ln, c, p.y + (float)i, p.z + (float)i);
+              if (r < (ris / total)) {
+                pdf = lpdf;
+                selected = true;
+              }
+            }
+          }
+          lw = (total / (float)n) / fmx(0.001f, pdf);
+        }
+
+        // ---- direct light, both shadow outcomes (raytrace_compute.glsl:233-246) ----
+        f3 sdir = mk(0.f, 0.f, 0.f);
+        float smax = 0.0f;
+        if (selected) {
+          const f3 toL = L.pos - p;
+          sdir = normalize(toL);
+          smax = length(toL);
+          if (rec.mat.useSpec) {
+            float li_;
+            const f3 bd = sample_direct_brdf(rec, Vv, L, li_);
+            q1 = (T * (((1.0f * L.color) * li_) * bd)) * lw;
+            q0 = (T * (((0.0f * L.color) * li_) * bd)) * lw;
+          } else {
+            const f3 Ld = light_dir(L, p);
+            const float fo = light_falloff(p, L);
+            const f3 lint = ((L.color * fo) * L.intensity) * lw;
+            const f3 tx = T * sample_direct_new(rec, Vv, Ld);
+            q1 = (tx * 1.0f) * lint;
+            q0 = (tx * 0.0f) * lint;
+          }
+        }
+
+        // ---- BRDF choice, Russian roulette, next direction (:248-285) ----
+        int type;
+        if (fixed_spec) {
+          type = SPECULAR_BRDF;
+        } else {
+          const float bp = brdf_probability(rec.mat, Vv, rec.normal);
+          if (u_bp < bp) {
+            type = SPECULAR_BRDF;
+            T = T / bp;
+          } else {
+            type = DIFFUSE_BRDF;
+            T = T / (1.0f - bp);
+          }
+        }
+        term = false;
+        if (rr) {
+          const float surv = clampf(luminance(T), 0.1f, 1.0f);
+          if (u_rr > surv) {
+            term = true;
+          } else {
+            T = T / surv;
+            randIndex++;
+          }
+        } else {
+          depth--;
+        }
+        if (!term) {
+          f3 dir, bw;
+          if (!sample_indirect(rec, Vv, type, r1, r2, dir, bw)) {
+            term = true;
+          } else {
+            T = T * bw;
+            nd = dir;
+          }
+        }
+
+        // The reference's loop has no depth cap (Russian roulette clamps the
+        // survival probability to >= 0.1).  A path still alive after 2^20
+        // bounces is cut (and counted) so a pathological scene cannot hang the GPU.
+        if (++bounces >= (1 << 20) && !term) {
+          term = true;
+          bump<COUNT>(c, ST_OVERFLOW);
+        }
+        ro = p;
+        if (selected) {  // trace CheckLightOccluded's ray next (t in (0.001, |light - p|))
+          rd = sdir;
+          tmax = smax;
+          shadow_phase = true;
+          start_ray();
+        } else if (term) {
+          finish_sample();
+        } else {
+          rd = nd;
+          tmax = __builtin_inff();
+          start_ray();
+        }
+      }
+    }
+  }
+  flush_counters<COUNT>(kp, c);
+}
+
+// Ordered sum of the sample buffer into the accumulation image (raytrace_compute.glsl:
+// 404-406 for frames frame_first .. frame_first + nframes - 1) and the sRGB8
+// image for accumFrames = out_frames (:412-413).
+__global__ __launch_bounds__(256) void accumulate_kernel(KParams kp, int out_frames) {
+  const int li = blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= kp.local_pixels) return;
+  const int ly = li / kp.W, x = li - ly * kp.W;
+  const int band = ly / kp.band_rows;
+  const int gy = (band * kp.nranks + kp.rank) * kp.band_rows + (ly - band * kp.band_rows);
+  if (x >= kp.ext_w || gy >= kp.ext_h) return;
   const float4 a0 = kp.accum[li];
   f3 acc = mk(a0.x, a0.y, a0.z);
+  const float4* L = kp.lbuf + li;
   for (int k = 0; k < kp.nframes; ++k) {
-    const int frame = kp.frame_first + k;
-    const int samp = frame % kp.WH;                              // raytrace_compute.glsl:400
-    const float2 nz = kp.noise_xy[(ln.base + samp) % kp.WH];     // SampleSquare, raytrace_utils.glsl:10-17
-    bump<COUNT>(c, ST_RNGSQ);
-    bump<COUNT>(c, ST_SAMPLES);
-    const float ox = nz.x - 0.5f, oy = nz.y - 0.5f;
-    const f3 ps = (p00 + du * ((float)x + ox)) + dv * ((float)gy + oy);   // GetRay :78-90
-    const f3 rd = ps - center;
-    acc = acc + ray_color<COUNT>(kp, ln, c, center, rd);
+    const float4 s = L[(size_t)k * (size_t)kp.local_pixels];
+    acc = acc + mk(s.x, s.y, s.z);
   }
   kp.accum[li] = make_float4(acc.x, acc.y, acc.z, 1.0f);
-  if (kp.write_output) {  // raytrace_compute.glsl:412-413
-    const f3 o = acc / (float)(kp.frame_first + kp.nframes - 1);
+  if (kp.write_output) {
+    const f3 o = acc / (float)out_frames;
     const uint32_t r = to_unorm8(linearToSrgb(o.x)), g = to_unorm8(linearToSrgb(o.y)),
                    b = to_unorm8(linearToSrgb(o.z));
     kp.out[li] = r | (g << 8) | (b << 16) | (255u << 24);
   }
-  flush_counters<COUNT>(kp, c);
+}
+
+// resetAccumBuffer (raytrace_compute.glsl:390-393)
+__global__ __launch_bounds__(256) void reset_kernel(KParams kp) {
+  const int li = blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= kp.local_pixels) return;
+  const int ly = li / kp.W, x = li - ly * kp.W;
+  const int band = ly / kp.band_rows;
+  const int gy = (band * kp.nranks + kp.rank) * kp.band_rows + (ly - band * kp.band_rows);
+  if (x >= kp.ext_w || gy >= kp.ext_h) return;
+  kp.accum[li] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
 }
 
 // The closest-hit test kernel of ray_intersects.glsl:135-161.
 __global__ __launch_bounds__(256) void closest_kernel(KParams kp, const srt_ray* rays, uint32_t n, uint32_t* hits,
                                                       float* tout) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Lane ln;
   ln.base = 0;
-  ln.stk = lds + threadIdx.x;
+  ln.stk = reinterpret_cast<uint32_t*>(g_smem) + threadIdx.x;
   ln.stride = blockDim.x;
   Counters c;
   for (int k = 0; k < ST_N; ++k) c.v[k] = 0;
@@ -715,13 +1045,36 @@ __global__ __launch_bounds__(256) void closest_kernel(KParams kp, const srt_ray*
   uint32_t hit = 0xFFFFFFFFu;
   for (uint32_t b = 0; b < kp.bvh_count; ++b) {
     const srt_bvh_record& rec = kp.bvhs[b];
-    const uint32_t h = traverse<false, true>(kp, ln, c, rec.first_index, xform(rec.frame, o, 1.0f),
-                                             xform(rec.frame, d, 0.0f), dist);
+    const uint32_t h = traverse<true, false>(kp, ln, c, rec.first_index, xform(rec.frame, o, 1.0f),
+                                      xform(rec.frame, d, 0.0f), dist, false);
     if (h != 0xFFFFFFFFu) hit = h;
   }
   hits[i] = hit;
   tout[i] = dist;
   flush_counters<true>(kp, c);
+}
+
+// Root-side assembly after the multi-GPU gather: gathered[r] holds rank r's
+// packed local rows (bands b with b % nranks == r, `rows_pad` rows each);
+// writes the full-frame accumulation image and its sRGB8 display image
+// (raytrace_compute.glsl:412-413 with accumFrames = `frames`).
+__global__ __launch_bounds__(256) void assemble_kernel(const float4* gathered, int nranks, int rows_pad, int W, int H,
+                                                       int band_rows, int frames, float4* accum, uint32_t* out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)W * (size_t)H) return;
+  const int y = (int)(i / (size_t)W), x = (int)(i - (size_t)y * W);
+  const int band = y / band_rows;
+  const int r = band % nranks;
+  const int lband = band / nranks;
+  const int ly = lband * band_rows + (y - band * band_rows);
+  const float4 a = gathered[((size_t)r * rows_pad + ly) * W + x];
+  if (accum) accum[i] = a;
+  if (out) {
+    const float inv = (float)frames;
+    const f3 o = mk(a.x, a.y, a.z) / inv;
+    const uint32_t rr = to_unorm8(linearToSrgb(o.x)), g = to_unorm8(linearToSrgb(o.y)), b = to_unorm8(linearToSrgb(o.z));
+    out[i] = rr | (g << 8) | (b << 16) | (255u << 24);
+  }
 }
 
 }  // namespace srt
@@ -769,10 +1122,14 @@ struct srt_context {
   float4* d_mats = nullptr;
   srt_bvh_record* d_bvhs = nullptr;
   uint32_t bvh_capacity = 0;
+  uint32_t bvh_uploaded = 0;   // records on the device (valid while !bvhs_dirty)
+  bool bvhs_dirty = true;
   std::vector<srt_bvh_record> h_bvhs;
   uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
   int stack_entries = 1;
   bool scene_ok = false;
+  bool lds_ok = false;        // scene indices fit the packed LDS stack entry
+  bool force_global = false;  // SRT_FORCE_GLOBAL_SCENE=1 disables LDS mode
   // lights
   std::vector<srt_light> h_lights;
   float4* d_lights = nullptr;
@@ -785,7 +1142,14 @@ struct srt_context {
   // images
   float4* d_accum = nullptr;
   uint32_t* d_out = nullptr;
+  bool images_external = false;
   int img_w = 0, img_rows = 0;
+  // sample buffer (nframes x local pixels float4)
+  float4* d_lbuf = nullptr;
+  size_t lbuf_bytes = 0;
+  size_t lbuf_cap = (size_t)16 << 30;  // SRT_SAMPLE_BUFFER_MB
+  int trav_frac16 = 8;                 // SRT_TRAV_FRAC16
+  int num_cus = 256;
   // stats
   unsigned long long* d_stats = nullptr;
   srt_stats stats{};
@@ -806,6 +1170,7 @@ int LocalRows(const srt_context* c, int H) {
 
 int EnsureBvhs(srt_context* c) {
   const uint32_t need = std::max<uint32_t>(c->bvh_count, 1);
+  if (!c->bvhs_dirty && c->bvh_uploaded >= need) return SRT_OK;
   std::vector<srt_bvh_record> recs(need);
   std::memset(recs.data(), 0, sizeof(srt_bvh_record) * need);   // bvhs[i >= n] read as zeros
   for (uint32_t i = 0; i < need && i < c->h_bvhs.size(); ++i) recs[i] = c->h_bvhs[i];
@@ -817,6 +1182,8 @@ int EnsureBvhs(srt_context* c) {
   }
   HIP_OK(hipMemcpyAsync(c->d_bvhs, recs.data(), sizeof(srt_bvh_record) * need, hipMemcpyHostToDevice, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
+  c->bvh_uploaded = need;
+  c->bvhs_dirty = false;
   return SRT_OK;
 }
 
@@ -908,25 +1275,84 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
   kp->nranks = c->nranks;
   kp->band_rows = c->band_rows;
   kp->local_rows = LocalRows(c, c->H);
+  kp->local_pixels = kp->local_rows * c->W;
   kp->ext_w = c->W;
   kp->ext_h = c->H;
   kp->stack_entries = c->stack_entries;
+  kp->nodes_f4 = (int)(2 * ((size_t)c->n_nodes + 1));
+  kp->tris_f4 = (int)(3 * (size_t)std::max<uint32_t>(c->n_tris, 1));
   CameraParams(c, kp);
   return SRT_OK;
 }
 
-int Launch(srt_context* c, srt::KParams& kp, bool count) {
-  const int block = 256;
-  const size_t lds = (size_t)block * 3 * sizeof(uint32_t) * (size_t)kp.stack_entries;
-  dim3 grid((kp.W + 15) / 16, (kp.local_rows + 15) / 16);
-  if (grid.x == 0 || grid.y == 0) return SRT_OK;
-  if (count) {
-    HIP_OK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_N, c->stream));
-    hipLaunchKernelGGL(srt::pathtrace_kernel<true>, grid, dim3(block), lds, c->stream, kp);
-  } else {
-    hipLaunchKernelGGL(srt::pathtrace_kernel<false>, grid, dim3(block), lds, c->stream, kp);
-  }
+// LDS budget per CU (gfx950: 160 KiB; one 1024-thread block per CU in LDS mode)
+constexpr size_t kLdsBytes = 160 * 1024;
+
+template <bool COUNT, bool LDSM>
+int LaunchSamples(srt_context* c, const srt::KParams& kp, int block, size_t lds) {
+  int per_cu = 0;
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sample_kernel<COUNT, LDSM>, block, lds));
+  per_cu = std::max(per_cu, 1);
+  const int blocks = c->num_cus * per_cu;
+  hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM>), dim3(blocks), dim3(block), lds, c->stream, kp);
   HIP_OK(hipGetLastError());
+  return SRT_OK;
+}
+
+// Runs frames kp.frame_first .. + kp.nframes - 1 (or the reset frame) through
+// sample_kernel + accumulate_kernel, in chunks that fit the sample buffer.
+int Launch(srt_context* c, srt::KParams& kp, bool count) {
+  const int npx = kp.local_pixels;
+  if (npx <= 0) return SRT_OK;
+  const dim3 pgrid((unsigned)((npx + 255) / 256));
+  if (kp.reset) {
+    hipLaunchKernelGGL(srt::reset_kernel, pgrid, dim3(256), 0, c->stream, kp);
+    HIP_OK(hipGetLastError());
+    return SRT_OK;
+  }
+  if (kp.nframes <= 0) return SRT_OK;
+  // LDS mode: the whole scene + 1024 lanes' 2-dword stacks fit in one CU's LDS
+  const size_t scene_bytes = ((size_t)kp.nodes_f4 + (size_t)kp.tris_f4) * sizeof(float4);
+  const size_t lds_mode_bytes = scene_bytes + (size_t)1024 * 2 * sizeof(uint32_t) * (size_t)kp.stack_entries;
+  const bool ldsm = kp.show_model && c->lds_ok && !c->force_global && lds_mode_bytes <= kLdsBytes;
+  const int block = ldsm ? 1024 : 256;
+  size_t lds;
+  if (ldsm) {
+    kp.stack_base_f4 = kp.nodes_f4 + kp.tris_f4;
+    lds = lds_mode_bytes;
+  } else {
+    kp.stack_base_f4 = 0;
+    lds = (size_t)block * 3 * sizeof(uint32_t) * (size_t)kp.stack_entries;
+  }
+  // sample buffer: as many frames per chunk as the buffer cap allows
+  const size_t per_frame = (size_t)npx * sizeof(float4);
+  const int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)kp.nframes, c->lbuf_cap / per_frame));
+  const size_t need = per_frame * (size_t)chunk;
+  if (need > c->lbuf_bytes) {
+    FreeDev(c->d_lbuf);
+    c->d_lbuf = nullptr;
+    c->lbuf_bytes = 0;
+    HIP_OK(hipMalloc(&c->d_lbuf, need));
+    c->lbuf_bytes = need;
+  }
+  kp.lbuf = c->d_lbuf;
+  kp.trav_frac16 = c->trav_frac16;
+  if (count) HIP_OK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_N, c->stream));
+  const int out_frames = kp.frame_first + kp.nframes - 1;
+  for (int f0 = 0; f0 < kp.nframes; f0 += chunk) {
+    srt::KParams kc = kp;
+    kc.frame_first = kp.frame_first + f0;
+    kc.nframes = std::min(chunk, kp.nframes - f0);
+    kc.write_output = (f0 + chunk >= kp.nframes) ? kp.write_output : 0;
+    int rc;
+    if (count && ldsm) rc = LaunchSamples<true, true>(c, kc, block, lds);
+    else if (count) rc = LaunchSamples<true, false>(c, kc, block, lds);
+    else if (ldsm) rc = LaunchSamples<false, true>(c, kc, block, lds);
+    else rc = LaunchSamples<false, false>(c, kc, block, lds);
+    if (rc) return rc;
+    hipLaunchKernelGGL(srt::accumulate_kernel, pgrid, dim3(256), 0, c->stream, kc, out_frames);
+    HIP_OK(hipGetLastError());
+  }
   if (count) {
     unsigned long long s[srt::ST_N];
     HIP_OK(hipMemcpyAsync(s, c->d_stats, sizeof(s), hipMemcpyDeviceToHost, c->stream));
@@ -997,6 +1423,14 @@ int srt_create(int device, void* stream, srt_context** out) {
   HIP_OK(hipSetDevice(device));
   auto* c = new srt_context();
   c->device = device;
+  if (const char* e = std::getenv("SRT_FORCE_GLOBAL_SCENE")) c->force_global = e[0] == '1';
+  if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_MB")) c->lbuf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
+  if (const char* e = std::getenv("SRT_TRAV_FRAC16")) c->trav_frac16 = std::max(0, std::min(16, std::atoi(e)));
+  {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+      c->num_cus = prop.multiProcessorCount;
+  }
   if (stream) {
     c->stream = static_cast<hipStream_t>(stream);
   } else {
@@ -1023,7 +1457,8 @@ int srt_destroy(srt_context* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   FreeDev(c->d_nodes); FreeDev(c->d_tris); FreeDev(c->d_mats); FreeDev(c->d_bvhs); FreeDev(c->d_lights);
-  FreeDev(c->d_noise_xy); FreeDev(c->d_noise_u); FreeDev(c->d_accum); FreeDev(c->d_out); FreeDev(c->d_stats);
+  FreeDev(c->d_noise_xy); FreeDev(c->d_noise_u); FreeDev(c->d_stats); FreeDev(c->d_lbuf);
+  if (!c->images_external) { FreeDev(c->d_accum); FreeDev(c->d_out); }
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return SRT_OK;
@@ -1211,10 +1646,14 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   HIP_OK(hipMemcpyAsync(c->d_tris, ht.data(), ht.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
   c->h_bvhs.assign(bvhs, bvhs + n_bvhs);
+  c->bvhs_dirty = true;
   c->n_nodes = n_nodes;
   c->n_tris = n_tris;
   c->n_mats = n_mats;
   c->stack_entries = depth + 1;
+  uint32_t max_leaf = 0;
+  for (uint32_t i = 0; i < n_nodes; ++i) max_leaf = std::max(max_leaf, nodes[i].prim_count);
+  c->lds_ok = n_tris < (1u << 24) && n_nodes < (1u << 24) && max_leaf < 256;
   c->scene_ok = true;
   if (c->bvh_count == 0) c->bvh_count = n_bvhs;
   // the zero records beyond n_bvhs traverse from node 0 with a zero ray
@@ -1229,6 +1668,7 @@ int srt_update_model_matrix(srt_context* c, uint32_t index, const float frame[16
     return SRT_ERR_INVALID;
   }
   std::memcpy(c->h_bvhs[index].frame, frame, sizeof(float) * 16);
+  c->bvhs_dirty = true;
   return SRT_OK;  // pushed to the device at the next launch (EnsureBvhs)
 }
 
@@ -1266,7 +1706,8 @@ int srt_alloc_images(srt_context* c) {
   HIP_OK(hipSetDevice(c->device));
   const int rows = LocalRows(c, c->H);
   const size_t px = (size_t)c->W * (size_t)std::max(rows, 1);
-  FreeDev(c->d_accum); FreeDev(c->d_out);
+  if (!c->images_external) { FreeDev(c->d_accum); FreeDev(c->d_out); }
+  c->images_external = false;
   c->d_accum = nullptr; c->d_out = nullptr;
   HIP_OK(hipMalloc(&c->d_accum, px * sizeof(float4)));
   HIP_OK(hipMalloc(&c->d_out, px * sizeof(uint32_t)));
@@ -1302,6 +1743,29 @@ int srt_read_output(srt_context* c, uint8_t* host, size_t bytes) {
   if (bytes < need) return SRT_ERR_INVALID;
   HIP_OK(hipMemcpyAsync(host, c->d_out, need, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
+  return SRT_OK;
+}
+
+int srt_set_image_buffers(srt_context* c, void* accum_dev, void* out_dev) {
+  if (!c || !accum_dev || !out_dev || c->W <= 0 || c->H <= 0) return SRT_ERR_INVALID;
+  if (!c->images_external) { FreeDev(c->d_accum); FreeDev(c->d_out); }
+  c->d_accum = static_cast<float4*>(accum_dev);
+  c->d_out = static_cast<uint32_t*>(out_dev);
+  c->images_external = true;
+  c->img_w = c->W;
+  c->img_rows = LocalRows(c, c->H);
+  return SRT_OK;
+}
+
+int srt_assemble_bands(srt_context* c, const void* gathered, int nranks, int rows_pad, int frames, void* accum_full,
+                       void* out_full) {
+  if (!c || !gathered || nranks < 1 || rows_pad < 1 || frames < 1 || c->W <= 0 || c->H <= 0) return SRT_ERR_INVALID;
+  HIP_OK(hipSetDevice(c->device));
+  const size_t n = (size_t)c->W * (size_t)c->H;
+  hipLaunchKernelGGL(srt::assemble_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream,
+                     static_cast<const float4*>(gathered), nranks, rows_pad, c->W, c->H, c->band_rows, frames,
+                     static_cast<float4*>(accum_full), static_cast<uint32_t*>(out_full));
+  HIP_OK(hipGetLastError());
   return SRT_OK;
 }
 

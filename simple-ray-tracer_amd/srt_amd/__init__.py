@@ -342,6 +342,15 @@ class Compute:
         check(lib().srt_image_pointers(self.ctx, C.byref(a), C.byref(o)), "image_pointers")
         return a.value or 0, o.value or 0
 
+    def set_image_buffers(self, accum_dev: int, out_dev: int):
+        check(lib().srt_set_image_buffers(self.ctx, C.c_void_p(accum_dev), C.c_void_p(out_dev)), "set_image_buffers")
+
+    def assemble_bands(self, gathered_dev: int, nranks: int, rows_pad: int, frames: int, accum_full_dev: int | None,
+                       out_full_dev: int | None):
+        check(lib().srt_assemble_bands(self.ctx, C.c_void_p(gathered_dev), nranks, rows_pad, frames,
+                                       C.c_void_p(accum_full_dev) if accum_full_dev else None,
+                                       C.c_void_p(out_full_dev) if out_full_dev else None), "assemble_bands")
+
     # -- dispatch -------------------------------------------------------------
     def Dispatch(self, groups_x: int, groups_y: int, groups_z: int = 1):
         """glDispatchCompute(groups_x, groups_y, 1) (src/main.cpp:706)."""

@@ -41,3 +41,5 @@ if __name__ == '__main__':
     gpu = '--cpu' not in sys.argv
     run('spheres', 64, 64, 2, gpu)
     run('rubik', 64, 64, 2, gpu)
+    run('rubik', 120, 72, 6, gpu)
+    run('spheres', 72, 120, 4, gpu)
