@@ -695,8 +695,8 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
   return __popcll(mask & ((1ull << lane) - 1ull));
 }
 
-template <bool COUNT, bool LDSM>
-__global__ __launch_bounds__(LDSM ? 1024 : 256) void sample_kernel(KParams kp) {
+template <bool COUNT, bool LDSM, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void sample_kernel(KParams kp) {
   const int tid = threadIdx.x;
   if constexpr (LDSM) {  // the block copies the scene (nodes + triangles) into LDS once
     const int total = kp.nodes_f4 + kp.tris_f4;
@@ -1148,7 +1148,8 @@ struct srt_context {
   float4* d_lbuf = nullptr;
   size_t lbuf_bytes = 0;
   size_t lbuf_cap = (size_t)16 << 30;  // SRT_SAMPLE_BUFFER_MB
-  int trav_frac16 = 8;                 // SRT_TRAV_FRAC16
+  int trav_frac16 = 10;                // SRT_TRAV_FRAC16 (measured best on Rubik 1080p: 8..10)
+  int lds_block = 1024;                // SRT_LDS_BLOCK (512 or 1024 threads per block in LDS mode)
   int num_cus = 256;
   // stats
   unsigned long long* d_stats = nullptr;
@@ -1288,13 +1289,13 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
 // LDS budget per CU (gfx950: 160 KiB; one 1024-thread block per CU in LDS mode)
 constexpr size_t kLdsBytes = 160 * 1024;
 
-template <bool COUNT, bool LDSM>
-int LaunchSamples(srt_context* c, const srt::KParams& kp, int block, size_t lds) {
+template <bool COUNT, bool LDSM, int BLOCK>
+int LaunchSamples(srt_context* c, const srt::KParams& kp, size_t lds) {
   int per_cu = 0;
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sample_kernel<COUNT, LDSM>, block, lds));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sample_kernel<COUNT, LDSM, BLOCK>, BLOCK, lds));
   per_cu = std::max(per_cu, 1);
   const int blocks = c->num_cus * per_cu;
-  hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM>), dim3(blocks), dim3(block), lds, c->stream, kp);
+  hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM, BLOCK>), dim3(blocks), dim3(BLOCK), lds, c->stream, kp);
   HIP_OK(hipGetLastError());
   return SRT_OK;
 }
@@ -1313,9 +1314,10 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   if (kp.nframes <= 0) return SRT_OK;
   // LDS mode: the whole scene + 1024 lanes' 2-dword stacks fit in one CU's LDS
   const size_t scene_bytes = ((size_t)kp.nodes_f4 + (size_t)kp.tris_f4) * sizeof(float4);
-  const size_t lds_mode_bytes = scene_bytes + (size_t)1024 * 2 * sizeof(uint32_t) * (size_t)kp.stack_entries;
+  const int lds_block = c->lds_block;
+  const size_t lds_mode_bytes = scene_bytes + (size_t)lds_block * 2 * sizeof(uint32_t) * (size_t)kp.stack_entries;
   const bool ldsm = kp.show_model && c->lds_ok && !c->force_global && lds_mode_bytes <= kLdsBytes;
-  const int block = ldsm ? 1024 : 256;
+  const int block = ldsm ? lds_block : 256;
   size_t lds;
   if (ldsm) {
     kp.stack_base_f4 = kp.nodes_f4 + kp.tris_f4;
@@ -1345,10 +1347,10 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
     kc.nframes = std::min(chunk, kp.nframes - f0);
     kc.write_output = (f0 + chunk >= kp.nframes) ? kp.write_output : 0;
     int rc;
-    if (count && ldsm) rc = LaunchSamples<true, true>(c, kc, block, lds);
-    else if (count) rc = LaunchSamples<true, false>(c, kc, block, lds);
-    else if (ldsm) rc = LaunchSamples<false, true>(c, kc, block, lds);
-    else rc = LaunchSamples<false, false>(c, kc, block, lds);
+    if (count && ldsm) rc = block == 512 ? LaunchSamples<true, true, 512>(c, kc, lds) : LaunchSamples<true, true, 1024>(c, kc, lds);
+    else if (count) rc = LaunchSamples<true, false, 256>(c, kc, lds);
+    else if (ldsm) rc = block == 512 ? LaunchSamples<false, true, 512>(c, kc, lds) : LaunchSamples<false, true, 1024>(c, kc, lds);
+    else rc = LaunchSamples<false, false, 256>(c, kc, lds);
     if (rc) return rc;
     hipLaunchKernelGGL(srt::accumulate_kernel, pgrid, dim3(256), 0, c->stream, kc, out_frames);
     HIP_OK(hipGetLastError());
@@ -1425,6 +1427,7 @@ int srt_create(int device, void* stream, srt_context** out) {
   c->device = device;
   if (const char* e = std::getenv("SRT_FORCE_GLOBAL_SCENE")) c->force_global = e[0] == '1';
   if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_MB")) c->lbuf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
+  if (const char* e = std::getenv("SRT_LDS_BLOCK")) c->lds_block = std::atoi(e) == 512 ? 512 : 1024;
   if (const char* e = std::getenv("SRT_TRAV_FRAC16")) c->trav_frac16 = std::max(0, std::min(16, std::atoi(e)));
   {
     hipDeviceProp_t prop;

@@ -11,7 +11,7 @@ import os
 import pathlib
 
 PKG_DIR = pathlib.Path(__file__).resolve().parent.parent
-LIB_PATH = PKG_DIR / "libsrt_amd.so"
+LIB_PATH = pathlib.Path(os.environ.get("SRT_LIB_PATH", PKG_DIR / "libsrt_amd.so"))
 
 SRT_OK = 0
 SRT_ERR_INVALID = 1
