@@ -175,7 +175,7 @@ def main():
             dist.gather(accum_local, gathered if rank == 0 else None, dst=0)
             if rank == 0:
                 torch.stack(gathered, out=gathered_flat)
-                c.assemble_bands(gathered_flat.data_ptr(), world, rows_pad, spp + 1, full_accum.data_ptr(),
+                c.assemble_bands(gathered_flat.data_ptr(), world, rows_pad, args.band_rows, spp + 1, full_accum.data_ptr(),
                                  full_out.data_ptr())
 
     for _ in range(args.warmup):

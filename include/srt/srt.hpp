@@ -1,0 +1,266 @@
+// srt/srt.hpp -- C++ host API of the MI355X path tracer, shaped like the reference's.
+//
+// Header-only layer over the C ABI (include/srt_amd.h) that keeps the names,
+// argument meaning and call pattern of matteobir12/simple-ray-tracer's host code
+// for this path, so src/main.cpp's per-frame loop ports line for line:
+//   Graphics::Compute            include/graphics/shader.h:46-55, src/graphics/Shader.cpp
+//   AssetUtils::LoadObject       src/asset_utils/model_loader.cpp:20-32
+//   AssetUtils::UploadModelDataToGPU / UpdateModelMatrix / UpdateRays
+//                                src/asset_utils/gpu_loader.cpp:63-210
+//   RayTracer::Camera / PointLight   src/raytracer/camera.cpp, include/raytracer/light.h
+// GL's "currently bound program" is mirrored by Compute::Use(): the upload
+// functions act on the last used Compute, as they act on the bound GL state.
+// Errors: std::runtime_error (the reference std::terminate()s in Init and
+// throws std::runtime_error("Model was null!") in the upload).
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <cstdio>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../srt_amd.h"
+
+namespace srt {
+
+struct vec3 {
+  float x = 0.f, y = 0.f, z = 0.f;
+};
+
+inline void check(int code, const char* what) {
+  if (code != SRT_OK) throw std::runtime_error(std::string(what) + ": " + srt_last_error());
+}
+
+namespace Graphics {
+
+class Compute;
+namespace detail {
+inline Compute*& current() {
+  static thread_local Compute* c = nullptr;
+  return c;
+}
+}  // namespace detail
+
+// Graphics::Compute: the raytrace_compute program.  `path` is kept for
+// interface parity; the kernel is built in (HIP code object for gfx950).
+class Compute {
+ public:
+  explicit Compute(const char* path, int device = 0, void* hip_stream = nullptr)
+      : path_(path ? path : ""), device_(device), stream_(hip_stream) {}
+  ~Compute() {
+    if (detail::current() == this) detail::current() = nullptr;
+    if (ctx_) srt_destroy(ctx_);
+  }
+  Compute(const Compute&) = delete;
+  Compute& operator=(const Compute&) = delete;
+
+  void Init() {
+    if (!ctx_) check(srt_create(device_, stream_, &ctx_), "Compute::Init");
+  }
+  void Use() {
+    Init();
+    detail::current() = this;
+  }
+  srt_context* context() {
+    Init();
+    return ctx_;
+  }
+
+  void SetBool(const std::string& name, bool v) {
+    const int rc = srt_set_bool(context(), name.c_str(), v ? 1 : 0);
+    if (rc == SRT_ERR_NOT_FOUND) {
+      if (name != "resetAccumBuffer")  // Shader.cpp:170-176
+        std::fprintf(stderr, "Warning: Uniform '%s' not found in compute shader\n", name.c_str());
+      return;
+    }
+    check(rc, "SetBool");
+  }
+  void SetInt(const std::string& name, int v) {  // unknown names are silently ignored (Shader.cpp:190-205)
+    const int rc = srt_set_int(context(), name.c_str(), v);
+    if (rc != SRT_ERR_NOT_FOUND) check(rc, "SetInt");
+    if (rc == SRT_OK && (name == "Width" || name == "Height")) images_dirty_ = true;
+  }
+  void SetUInt(const std::string& name, uint32_t v) {
+    const int rc = srt_set_uint(context(), name.c_str(), v);
+    if (rc != SRT_ERR_NOT_FOUND) check(rc, "SetUInt");
+  }
+  void SetFloat(const std::string& name, float v) {
+    const int rc = srt_set_float(context(), name.c_str(), v);
+    if (rc != SRT_ERR_NOT_FOUND) check(rc, "SetFloat");
+  }
+  void SetVec3(const std::string& name, const vec3& v) {
+    const int rc = srt_set_vec3(context(), name.c_str(), v.x, v.y, v.z);
+    if (rc != SRT_ERR_NOT_FOUND) check(rc, "SetVec3");
+  }
+
+  // texel buffers at units 1, 2 (src/main.cpp:269-301) and the light SSBO (binding 4)
+  void BindNoise(const std::vector<float>& noise_rgb, const std::vector<float>& noise_uniform_rgb) {
+    if (noise_rgb.size() != noise_uniform_rgb.size() || noise_rgb.size() % 3) throw std::runtime_error("BindNoise");
+    check(srt_set_noise(context(), noise_rgb.data(), noise_uniform_rgb.data(), noise_rgb.size() / 3), "BindNoise");
+  }
+  void BindLights(const std::vector<srt_light>& lights) {
+    check(srt_set_lights(context(), lights.data(), (uint32_t)lights.size()), "BindLights");
+  }
+
+  // glDispatchCompute(gx, gy, 1) (src/main.cpp:706); images 0/3 follow Width x Height
+  void Dispatch(uint32_t gx, uint32_t gy, uint32_t gz = 1) {
+    if (gz != 1) throw std::runtime_error("Dispatch: groups_z must be 1");
+    if (images_dirty_) {
+      check(srt_alloc_images(context()), "alloc images");
+      images_dirty_ = false;
+    }
+    check(srt_dispatch(context(), gx, gy), "Dispatch");
+  }
+  // glMemoryBarrier + glFinish (src/main.cpp:709-718)
+  void Finish() { check(srt_finish(context()), "Finish"); }
+
+  // `n` progressive frames in one launch (same accumulation as n Dispatch calls)
+  void RenderFrames(int frame_first, int n, bool write_output = true) {
+    if (images_dirty_) {
+      check(srt_alloc_images(context()), "alloc images");
+      images_dirty_ = false;
+    }
+    check(srt_render_frames(context(), frame_first, n, write_output ? 1 : 0, 0), "RenderFrames");
+  }
+  std::vector<float> ReadAccum() {
+    std::vector<float> v((size_t)srt_local_rows(context()) * width() * 4);
+    check(srt_read_accum(context(), v.data(), v.size() * sizeof(float)), "ReadAccum");
+    return v;
+  }
+  std::vector<uint8_t> ReadOutput() {
+    std::vector<uint8_t> v((size_t)srt_local_rows(context()) * width() * 4);
+    check(srt_read_output(context(), v.data(), v.size()), "ReadOutput");
+    return v;
+  }
+  void SetWidthHint(int w) { width_ = w; }
+  int width() const { return width_; }
+
+ private:
+  std::string path_;
+  int device_;
+  void* stream_;
+  srt_context* ctx_ = nullptr;
+  bool images_dirty_ = true;
+  int width_ = 0;
+};
+
+}  // namespace Graphics
+
+namespace AssetUtils {
+
+// AssetUtils::Model (asset_utils/types.h:39-52), owned on the host.
+class Model {
+ public:
+  explicit Model(srt_model* m) : m_(m) {}
+  ~Model() { srt_model_free(m_); }
+  Model(const Model&) = delete;
+  Model& operator=(const Model&) = delete;
+  srt_model* handle() const { return m_; }
+
+ private:
+  srt_model* m_;
+};
+
+// model_loader.cpp:20-32: objects/<name>/<name>.obj
+inline std::unique_ptr<Model> LoadObject(const std::string& name, const std::string& objects_dir = "./objects/") {
+  srt_model* m = nullptr;
+  check(srt_model_load((objects_dir + name + "/" + name + ".obj").c_str(), &m), "LoadObject");
+  return std::make_unique<Model>(m);
+}
+
+// gpu_loader.cpp:63-183, into the last used Compute (the bound program).
+inline void UploadModelDataToGPU(const std::vector<Model*>& models, const uint32_t binding_offset = 0) {
+  (void)binding_offset;  // bindings are fixed by the C ABI
+  Graphics::Compute* c = Graphics::detail::current();
+  if (!c) throw std::runtime_error("UploadModelDataToGPU: no Compute in use");
+  std::vector<const srt_model*> hs;
+  for (Model* m : models) {
+    if (!m) throw std::runtime_error("Model was null!");
+    hs.push_back(m->handle());
+  }
+  srt_scene* s = nullptr;
+  check(srt_scene_build(hs.data(), (uint32_t)hs.size(), &s), "UploadModelDataToGPU");
+  const int rc = srt_upload_scene_obj(c->context(), s);
+  srt_scene_free(s);
+  check(rc, "UploadModelDataToGPU");
+}
+
+// gpu_loader.cpp:185-196 (glm::mat4 column-major, m[c * 4 + r])
+inline void UpdateModelMatrix(const uint32_t index, const std::array<float, 16>& matrix) {
+  Graphics::Compute* c = Graphics::detail::current();
+  if (!c) throw std::runtime_error("UpdateModelMatrix: no Compute in use");
+  check(srt_update_model_matrix(c->context(), index, matrix.data()), "UpdateModelMatrix");
+}
+
+// gpu_loader.cpp:198-210 + the ray_intersects.glsl test kernel: closest hit per ray
+inline std::vector<uint32_t> UpdateRaysAndTrace(const std::vector<srt_ray>& rays, std::vector<float>* t_out = nullptr) {
+  Graphics::Compute* c = Graphics::detail::current();
+  if (!c) throw std::runtime_error("UpdateRays: no Compute in use");
+  std::vector<uint32_t> hits(rays.size());
+  std::vector<float> t(rays.size());
+  check(srt_trace_closest(c->context(), rays.data(), (uint32_t)rays.size(), hits.data(), t.data()), "UpdateRays");
+  if (t_out) *t_out = std::move(t);
+  return hits;
+}
+
+}  // namespace AssetUtils
+
+namespace RayTracer {
+
+// raytracer/light.h:54-63
+inline srt_light PointLight(const vec3& position, const vec3& color, float intensity) {
+  srt_light l{};
+  l.position[0] = position.x; l.position[1] = position.y; l.position[2] = position.z;
+  l.color[0] = color.x; l.color[1] = color.y; l.color[2] = color.z;
+  l.intensity = intensity;
+  return l;
+}
+
+// Camera basis vectors as uploaded by src/main.cpp:672-675
+class Camera {
+ public:
+  explicit Camera(bool show_model) : show_model_(show_model) { Reset(); }
+  void Reset() {
+    float o[3], f[3], u[3], r[3];
+    check(srt_camera_reset(show_model_ ? 1 : 0, o, f, u, r), "Camera::Reset");
+    position_ = {o[0], o[1], o[2]}; front_ = {f[0], f[1], f[2]}; up_ = {u[0], u[1], u[2]}; right_ = {r[0], r[1], r[2]};
+    yaw_ = -90.0f;
+    pitch_ = 0.0f;
+  }
+  void Rotate(float yaw_offset, float pitch_offset) {
+    yaw_ += yaw_offset;
+    pitch_ += pitch_offset;
+    if (pitch_ > 89.0f) pitch_ = 89.0f;
+    if (pitch_ < -89.0f) pitch_ = -89.0f;
+    float f[3], u[3], r[3];
+    check(srt_camera_basis(yaw_, pitch_, f, u, r), "Camera::Rotate");
+    front_ = {f[0], f[1], f[2]}; up_ = {u[0], u[1], u[2]}; right_ = {r[0], r[1], r[2]};
+  }
+  vec3 getOrigin() const { return position_; }
+  vec3 getForward() const { return front_; }
+  vec3 getUpVector() const { return up_; }
+  vec3 getRightVector() const { return right_; }
+
+ private:
+  bool show_model_;
+  vec3 position_, front_, up_, right_;
+  float yaw_ = -90.0f, pitch_ = 0.0f;
+};
+
+}  // namespace RayTracer
+
+namespace Common {
+// UpdateNoiseTex's buffers (src/main.cpp:269-301): W*H unit vectors, then W*H uniform vec3s
+inline void GenerateNoise(uint32_t width, uint32_t height, std::vector<float>* noise, std::vector<float>* noise_uniform,
+                          bool gcc_order = true) {
+  const size_t n = (size_t)width * height;
+  noise->resize(3 * n);
+  noise_uniform->resize(3 * n);
+  check(srt_noise_generate((uint32_t)n, gcc_order ? 1 : 0, noise->data(), noise_uniform->data()), "GenerateNoise");
+}
+}  // namespace Common
+
+}  // namespace srt

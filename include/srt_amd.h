@@ -137,10 +137,11 @@ int srt_image_pointers(srt_context* ctx, void** accum_dev, void** out_dev);
  * image3 / image0, e.g. tensors an RCCL gather reads from. */
 int srt_set_image_buffers(srt_context* ctx, void* accum_dev, void* out_dev);
 /* Root side of the multi-GPU frame: `gathered` holds nranks blocks of
- * rows_pad packed local rows (rank order); writes the full-frame RGBA32F
- * accumulation image and sRGB8 image for accumFrames = `frames` (either
- * output may be NULL).  Enqueued on the context's stream. */
-int srt_assemble_bands(srt_context* ctx, const void* gathered, int nranks, int rows_pad, int frames,
+ * rows_pad packed local rows (rank order, bands of band_rows rows dealt
+ * round-robin); writes the full-frame (Width x Height) RGBA32F accumulation
+ * image and sRGB8 image for accumFrames = `frames` (either output may be
+ * NULL).  Enqueued on the context's stream. */
+int srt_assemble_bands(srt_context* ctx, const void* gathered, int nranks, int rows_pad, int band_rows, int frames,
                        void* accum_full, void* out_full);
 
 /* Closest-hit query: the test kernel ray_intersects.glsl:135-161 fed through

@@ -1427,6 +1427,7 @@ int srt_create(int device, void* stream, srt_context** out) {
   c->device = device;
   if (const char* e = std::getenv("SRT_FORCE_GLOBAL_SCENE")) c->force_global = e[0] == '1';
   if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_MB")) c->lbuf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
+  if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_KB")) c->lbuf_cap = (size_t)std::max(1L, std::atol(e)) << 10;
   if (const char* e = std::getenv("SRT_LDS_BLOCK")) c->lds_block = std::atoi(e) == 512 ? 512 : 1024;
   if (const char* e = std::getenv("SRT_TRAV_FRAC16")) c->trav_frac16 = std::max(0, std::min(16, std::atoi(e)));
   {
@@ -1760,13 +1761,14 @@ int srt_set_image_buffers(srt_context* c, void* accum_dev, void* out_dev) {
   return SRT_OK;
 }
 
-int srt_assemble_bands(srt_context* c, const void* gathered, int nranks, int rows_pad, int frames, void* accum_full,
-                       void* out_full) {
-  if (!c || !gathered || nranks < 1 || rows_pad < 1 || frames < 1 || c->W <= 0 || c->H <= 0) return SRT_ERR_INVALID;
+int srt_assemble_bands(srt_context* c, const void* gathered, int nranks, int rows_pad, int band_rows, int frames,
+                       void* accum_full, void* out_full) {
+  if (!c || !gathered || nranks < 1 || rows_pad < 1 || band_rows < 1 || frames < 1 || c->W <= 0 || c->H <= 0)
+    return SRT_ERR_INVALID;
   HIP_OK(hipSetDevice(c->device));
   const size_t n = (size_t)c->W * (size_t)c->H;
   hipLaunchKernelGGL(srt::assemble_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream,
-                     static_cast<const float4*>(gathered), nranks, rows_pad, c->W, c->H, c->band_rows, frames,
+                     static_cast<const float4*>(gathered), nranks, rows_pad, c->W, c->H, band_rows, frames,
                      static_cast<float4*>(accum_full), static_cast<uint32_t*>(out_full));
   HIP_OK(hipGetLastError());
   return SRT_OK;

@@ -345,9 +345,9 @@ class Compute:
     def set_image_buffers(self, accum_dev: int, out_dev: int):
         check(lib().srt_set_image_buffers(self.ctx, C.c_void_p(accum_dev), C.c_void_p(out_dev)), "set_image_buffers")
 
-    def assemble_bands(self, gathered_dev: int, nranks: int, rows_pad: int, frames: int, accum_full_dev: int | None,
-                       out_full_dev: int | None):
-        check(lib().srt_assemble_bands(self.ctx, C.c_void_p(gathered_dev), nranks, rows_pad, frames,
+    def assemble_bands(self, gathered_dev: int, nranks: int, rows_pad: int, band_rows: int, frames: int,
+                       accum_full_dev: int | None, out_full_dev: int | None):
+        check(lib().srt_assemble_bands(self.ctx, C.c_void_p(gathered_dev), nranks, rows_pad, band_rows, frames,
                                        C.c_void_p(accum_full_dev) if accum_full_dev else None,
                                        C.c_void_p(out_full_dev) if out_full_dev else None), "assemble_bands")
 

@@ -99,7 +99,7 @@ _SIGS = {
     "srt_write_accum": (C.c_int, [P, P, C.c_size_t]),
     "srt_image_pointers": (C.c_int, [P, C.POINTER(P), C.POINTER(P)]),
     "srt_set_image_buffers": (C.c_int, [P, P, P]),
-    "srt_assemble_bands": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P]),
+    "srt_assemble_bands": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
     "srt_trace_closest": (C.c_int, [P, P, C.c_uint32, P, P]),
     "srt_model_load": (C.c_int, [C.c_char_p, C.POINTER(P)]),
     "srt_model_from_triangles": (C.c_int, [P, C.c_uint32, P, P, C.c_float, C.POINTER(P)]),

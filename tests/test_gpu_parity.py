@@ -1,0 +1,239 @@
+"""GPU parity: the HIP path tracer (through the C ABI) vs the CPU oracle, bit for bit.
+
+Bar: accumulation image bit-identical (NaN == NaN), RGBA8 image identical, CheckHit query
+counts identical, on seeded inputs small enough for the oracle; at BASELINE's full frame
+size, oracle rows sampled across the frame plus size-independent properties
+(determinism, chunking / LDS / tiling invariance).
+"""
+import os
+import pathlib
+import subprocess
+
+import numpy as np
+import pytest
+
+import srt_amd as S
+from srt_amd import render as R
+from conftest import OBJECTS, PKG, ROOT, bits_equal, oracle_render
+from oracle import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rubik():
+    return S.load_obj(OBJECTS / "Rubik" / "Rubik.obj")
+
+
+def gpu_render(setup, spp, *, per_frame=False, **kw):
+    r = R.Renderer(setup, **kw)
+    try:
+        if per_frame:
+            r.clear()
+            for _ in range(spp):
+                r.frame()
+        else:
+            r.render(spp, count=True)
+        r.finish()
+        return r.accum(), r.output(), r.compute.stats()
+    finally:
+        r.close()
+
+
+def assert_parity(setup, spp, **kw):
+    acc, out, st = oracle_render(setup, spp)
+    gacc, gout, gst = gpu_render(setup, spp, **kw)
+    eq = bits_equal(gacc, acc)
+    assert eq.all(), f"{(~eq).sum()} accumulation values differ"
+    assert (gout == out).all()
+    if not kw.get("per_frame"):
+        assert gst["rays"] == st["rays"] and gst["samples"] == st["samples"]
+        assert gst["stack_overflow"] == 0
+    return gacc, gout
+
+
+@pytest.mark.parametrize("w,h,spp,depth", [(64, 64, 2, 5), (72, 40, 3, 5), (40, 72, 2, 8), (33, 17, 2, 0)])
+def test_spheres_parity(w, h, spp, depth):
+    assert_parity(R.make_setup(w, h, show_model=False, max_depth=depth), spp)
+
+
+@pytest.mark.parametrize("w,h,spp,depth", [(64, 64, 2, 5), (96, 54, 4, 5), (40, 72, 2, 3), (31, 23, 3, 8)])
+def test_rubik_parity(rubik, w, h, spp, depth):
+    assert_parity(R.make_setup(w, h, show_model=True, models=[rubik], max_depth=depth), spp)
+
+
+def test_per_frame_dispatch_matches_fused(rubik):
+    setup = R.make_setup(48, 40, show_model=True, models=[rubik])
+    acc_f, out_f = assert_parity(setup, 3)
+    acc_d, out_d, _ = gpu_render(setup, 3, per_frame=True)
+    assert bits_equal(acc_d, acc_f).all() and (out_d == out_f).all()
+
+
+def test_partial_dispatch_extent(rubik):
+    """glDispatchCompute(gx, gy) covers only gx*8 x gy*8 invocations; other pixels keep their values."""
+    setup = R.make_setup(48, 40, show_model=True, models=[rubik])
+    acc, out, _ = oracle_render(setup, 1)
+    r = R.Renderer(setup)
+    try:
+        r.clear()
+        r.compute.write_accum(np.full((40, 48, 4), 7.0, np.float32))
+        c = r.compute
+        c.SetBool("resetAccumBuffer", True)
+        c.SetInt("accumFrames", 1)
+        c.Dispatch(3, 2)  # 24 x 16 pixels reset
+        c.SetBool("resetAccumBuffer", False)
+        c.SetInt("accumFrames", 2)
+        c.Dispatch(3, 2)
+        c.Finish()
+        g = c.read_accum()
+    finally:
+        r.close()
+    assert bits_equal(g[:16, :24], acc[:16, :24]).all()
+    assert (g[16:, :] == 7.0).all() and (g[:, 24:] == 7.0).all()
+
+
+def test_lights_edge_cases(rubik):
+    # lightCount larger than the SSBO (indices past it read zeros) and a single light
+    setup = R.make_setup(40, 32, show_model=True, models=[rubik])
+    assert_parity(setup, 2)
+    one = R.make_setup(40, 32, show_model=True, models=[rubik], lights=S.MODEL_LIGHTS[:1])
+    assert_parity(one, 2)
+    none = R.make_setup(32, 24, show_model=False, lights=())
+    assert_parity(none, 2)
+
+
+def test_ghost_bvh_count(rubik):
+    """src/main.cpp:683 sets bvh_count = 2 with one model: bvhs[1] is an out-of-bounds (zero) record."""
+    setup = R.make_setup(40, 32, show_model=True, models=[rubik], bvh_count=2)
+    acc2, out2 = assert_parity(setup, 2)
+    setup1 = R.make_setup(40, 32, show_model=True, models=[rubik], bvh_count=1)
+    acc1, _, _ = gpu_render(setup1, 2)
+    assert bits_equal(acc1, acc2).all()  # the zero record never hits
+
+
+def test_two_models_with_transform(rubik):
+    second = S.load_obj(OBJECTS / "Rubik" / "Rubik.obj")
+    setup = R.make_setup(48, 40, show_model=True, models=[rubik, second])
+    # move the second cube: world -> model frame translates by (-12, 2, 5)
+    frame = np.eye(4, dtype=np.float32)
+    frame[3, :3] = (12.0, -2.0, -5.0)  # glm column 3 = translation
+    setup.scene.bvhs[1]["frame"] = frame.reshape(16)
+    assert_parity(setup, 2)
+
+
+def test_textured_material_albedo(tmp_path):
+    import test_producers as P
+
+    w, h = 4, 4
+    px = [200, 100, 50] * (w * h)
+    P._write_png(tmp_path / "t.png", w, h, px)
+    (tmp_path / "m.mtl").write_text("newmtl tex\nKd 1 1 1\nKs 0.3 0.3 0.3\nNs 30\nmap_Kd t.png\n")
+    verts = "v -6 0 -6\nv 6 0 -6\nv 6 12 -6\nv -6 12 -6\n"
+    (tmp_path / "m.obj").write_text("mtllib m.mtl\n" + verts + "usemtl tex\nf 1 2 3 4\n")
+    setup = R.make_setup(32, 32, show_model=True, models=[S.load_obj(tmp_path / "m.obj")])
+    assert_parity(setup, 2)
+
+
+def test_synthetic_mesh_global_mode():
+    """A 30k-triangle mesh: too big for the LDS copy, exercises the global-memory traversal."""
+    setup = R.make_setup(40, 30, show_model=True, models=[R.synthetic_model(30000, seed=3)])
+    assert_parity(setup, 2)
+
+
+def test_lds_and_global_modes_agree(rubik, monkeypatch):
+    setup = R.make_setup(64, 48, show_model=True, models=[rubik])
+    a, o, _ = gpu_render(setup, 3)
+    monkeypatch.setenv("SRT_FORCE_GLOBAL_SCENE", "1")
+    b, p, _ = gpu_render(setup, 3)
+    assert bits_equal(a, b).all() and (o == p).all()
+
+
+def test_sample_buffer_chunking_invariance(rubik, monkeypatch):
+    setup = R.make_setup(64, 48, show_model=True, models=[rubik])
+    a, o, _ = gpu_render(setup, 9)
+    monkeypatch.setenv("SRT_SAMPLE_BUFFER_KB", "100")  # 2 frames of 64x48 per chunk -> 5 chunks
+    b, p, _ = gpu_render(setup, 9)
+    assert bits_equal(a, b).all() and (o == p).all()
+
+
+@pytest.mark.parametrize("nranks,band", [(2, 16), (3, 8)])
+def test_row_band_tiling_reassembles(rubik, nranks, band):
+    import torch
+
+    W, H = 64, 56
+    setup = R.make_setup(W, H, show_model=True, models=[rubik])
+    full, full_out, _ = gpu_render(setup, 3)
+    nb = (H + band - 1) // band
+    rows_pad = ((nb + nranks - 1) // nranks) * band
+    gathered = torch.zeros((nranks, rows_pad, W, 4), dtype=torch.float32, device="cuda")
+    for rank in range(nranks):
+        loc, _, _ = gpu_render(setup, 3, rank=rank, nranks=nranks, band_rows=band)
+        gathered[rank, :loc.shape[0]] = torch.from_numpy(loc).cuda()
+    torch.cuda.synchronize()
+    r = R.Renderer(setup)
+    try:
+        acc = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+        out = torch.empty((H, W), dtype=torch.int32, device="cuda")
+        r.compute.assemble_bands(gathered.data_ptr(), nranks, rows_pad, band, 4, acc.data_ptr(), out.data_ptr())
+        r.finish()
+        torch.cuda.synchronize()
+    finally:
+        r.close()
+    assert bits_equal(acc.cpu().numpy(), full).all()
+    assert (out.cpu().numpy().view(np.uint8).reshape(H, W, 4) == full_out).all()
+
+
+def _kat_rays(n, seed):
+    rng = np.random.default_rng(seed)
+    rays = np.zeros(n, S.RAY_DTYPE)
+    rays["o"] = rng.uniform([-15, -3, -15], [15, 22, 15], size=(n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d[::7, 0] = 0.0          # zero components: infinite 1/d in the slab test
+    d[::11, 1:] = 0.0
+    d[5] = 0.0               # the zero direction
+    rays["d"] = d
+    rays["t"] = np.where(np.arange(n) % 5 == 0, np.float32(3.0), np.float32(1e30))
+    rays[0]["o"], rays[0]["d"] = (-10.0, 3.0, 6.0), np.array([0.9838, -0.0118, 0.1787], np.float32)
+    rays[1]["o"], rays[1]["d"] = (0.0, 0.0, 0.0), (0.0, 1.0, 0.0)
+    return rays
+
+
+def test_trace_closest_matches_oracle(rubik):
+    scene = S.Scene.from_models([rubik])
+    rays = _kat_rays(20000, 11)
+    hits_o, t_o, _, st = O.Oracle(scene).trace_closest(1, rays)
+    c = S.Compute().Init()
+    try:
+        c.bind_scene(scene)
+        c.SetUInt("bvh_count", 1)
+        hits, t = c.trace_closest(rays)
+    finally:
+        c.close()
+    assert hits[0] == 365 and hits[1] != 0xFFFFFFFF
+    assert (hits == hits_o).all()
+    assert bits_equal(t, t_o).all()
+    assert (hits != 0xFFFFFFFF).sum() > 1000
+
+
+def test_full_frame_rows_and_determinism(rubik):
+    """BASELINE frame size (1920x1080): oracle rows sampled across the frame, bit-exact; two runs identical."""
+    W, H, spp = 1920, 1080, 2
+    setup = R.make_setup(W, H, show_model=True, models=[rubik])
+    a, o, st = gpu_render(setup, spp)
+    rows = np.arange(3, H, 97, dtype=np.int32)
+    acc, out, _ = oracle_render(setup, spp, rows=rows)
+    assert bits_equal(a[rows], acc[rows]).all()
+    assert (o[rows] == out[rows]).all()
+    b, p, st2 = gpu_render(setup, spp)
+    assert bits_equal(a, b).all() and (o == p).all() and st["rays"] == st2["rays"]
+    assert np.isfinite(a[..., :3]).mean() > 0.999 and (a[..., 3] == 1.0).all()
+
+
+def test_cpp_api_program():
+    """The C++ mirror API running the reference's integration test + main loop (tests/cpp/test_api.cpp)."""
+    exe = ROOT / "tests" / "cpp" / "_build" / "test_api"
+    exe.parent.mkdir(exist_ok=True)
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I", str(ROOT / "include"), str(ROOT / "tests/cpp/test_api.cpp"),
+                    "-o", str(exe), "-L", str(PKG), "-lsrt_amd", f"-Wl,-rpath,{PKG}"], check=True)
+    res = subprocess.run([str(exe), str(OBJECTS) + "/"], capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0 and res.stdout.startswith("OK"), res.stdout + res.stderr

@@ -1,0 +1,217 @@
+"""Scene producers (host C++, libsrt_amd.so) vs the reference's known answers and vs an independent
+Python restatement (oracle/scene_ref.py) -- bit for bit.  CPU only: no GPU call is made."""
+import math
+import pathlib
+
+import numpy as np
+import pytest
+
+import srt_amd as S
+from oracle import scene_ref as R
+from conftest import OBJECTS
+
+RUBIK = OBJECTS / "Rubik" / "Rubik.obj"
+
+
+def test_rubik_ingest_known_answers():
+    """SURVEY.md 8c item 1 (re-execution of the reference loader + builder on Rubik.obj)."""
+    info = S.load_obj(RUBIK).info()
+    assert info["triangles"] == 1188
+    assert info["vertices"] == 3564
+    assert info["nodes"] == 427
+    assert info["leaves"] == 214
+    assert info["max_depth"] == 9
+    assert info["faces_dropped"] == 0
+    np.testing.assert_array_equal(info["root_min"], np.array([-9.0132, 0.0, -9.1173], np.float32))
+    np.testing.assert_array_equal(info["root_max"], np.array([9.1608, 18.3665, 9.1173], np.float32))
+
+
+def _scene_from_ref(models):
+    bvhs, nodes, mats, tris, verts = R.flatten(models)
+    return bvhs, nodes, mats, tris, verts
+
+
+def _compare_scene(sc: S.Scene, ref):
+    bvhs, nodes, mats, tris, verts = ref
+    assert len(sc.bvhs) == len(bvhs) and len(sc.nodes) == len(nodes) and len(sc.tris) == len(tris)
+    assert len(sc.verts) == len(verts) and len(sc.mats) == len(mats)
+    for i, (first, count) in enumerate(bvhs):
+        assert sc.bvhs[i]["first_index"] == first and sc.bvhs[i]["count"] == count
+        np.testing.assert_array_equal(sc.bvhs[i]["frame"], np.eye(4, dtype=np.float32).reshape(16))
+    ref_nodes = np.zeros(len(nodes), S.NODE_DTYPE)
+    for i, (mn, first, mx, count) in enumerate(nodes):
+        ref_nodes[i] = (np.array(mn, np.float32), first, np.array(mx, np.float32), count)
+    assert sc.nodes.tobytes() == ref_nodes.tobytes()
+    ref_tris = np.array([(t[:3], t[3]) for t in tris], S.TRI_DTYPE)
+    assert sc.tris.tobytes() == ref_tris.tobytes()
+    np.testing.assert_array_equal(sc.verts["pos"].view(np.uint32), np.array(verts, np.float32).view(np.uint32))
+    assert (sc.verts["uv"] == 0).all()  # has_texcoords is never set (asset_utils/types.h:105)
+    for i, (kd, ns, ks, use_tex) in enumerate(mats):
+        assert sc.mats[i]["diffuse"].tobytes() == np.array(kd, np.float32).tobytes()
+        assert sc.mats[i]["Ks"].tobytes() == np.array(ks, np.float32).tobytes()
+        assert np.float32(sc.mats[i]["Ns"]) == ns and sc.mats[i]["use_texture"] == use_tex
+
+
+def _ref_model(path):
+    packed, tris, mats, dropped = R.load_obj(path)
+    nodes, prims, depth = R.build_bvh(packed, tris)
+    return (packed, nodes, prims, mats), depth, dropped
+
+
+def test_rubik_arrays_match_independent_restatement():
+    ref_model, depth, dropped = _ref_model(RUBIK)
+    assert depth == 9 and dropped == 0
+    _compare_scene(S.Scene.from_models([S.load_obj(RUBIK)]), _scene_from_ref([ref_model]))
+
+
+def test_two_model_rebasing():
+    """Index rebasing across models (gpu_loader.cpp:107-130)."""
+    m1, _, _ = _ref_model(RUBIK)
+    m2, _, _ = _ref_model(RUBIK)
+    _compare_scene(S.Scene.from_models([S.load_obj(RUBIK), S.load_obj(RUBIK)]), _scene_from_ref([m1, m2]))
+
+
+def test_null_model_raises():
+    with pytest.raises(Exception):
+        S.Scene.from_models([None])
+
+
+OBJ_EDGE = """# edge cases of ParseOBJ (model_loader.cpp:35-177)
+mtllib edge.mtl\r
+v 0 0 0
+v 1 0 0
+v 1 1 0
+v 0 1 0
+v 0.5 0.5 1
+vt 0 0
+vn 0 0 1
+f 1 2 3
+usemtl red
+f 1/1/1 2/1/1 3/1/1 4/1/1
+f 1 2 3 4 5
+   f 1//1 3//1 5//1   \t
+usemtl missing
+f 2 3 5
+usemtl blue
+f 3 4 5
+"""
+MTL_EDGE = """newmtl red
+Kd 1 0 0
+Ks 0.5 0.5 0.5
+Ns 20
+newmtl blue
+Kd 0 0 1
+newmtl red
+Kd 0 1 0
+"""
+
+
+def test_obj_parser_edge_cases(tmp_path):
+    (tmp_path / "edge.obj").write_text(OBJ_EDGE)
+    (tmp_path / "edge.mtl").write_text(MTL_EDGE)
+    m = S.load_obj(tmp_path / "edge.obj")
+    info = m.info()
+    # 1 face before the first usemtl joins 'red'; the quad is fanned to 2; the 5-gon is dropped;
+    # 1 face under 'missing' (index 0), 1 under 'blue'
+    assert info["triangles"] == 6 and info["faces_dropped"] == 1
+    ref_model, _, dropped = _ref_model(tmp_path / "edge.obj")
+    assert dropped == 1
+    sc = S.Scene.from_models([m])
+    _compare_scene(sc, _scene_from_ref([ref_model]))
+    # the duplicate 'newmtl red' left the parser on 'blue', whose Kd became (0,1,0)
+    assert sc.mats[1]["diffuse"].tolist() == [0.0, 1.0, 0.0]
+
+
+def test_synthetic_mesh_bvh_matches():
+    from srt_amd.render import synthetic_triangles
+
+    xyz9 = synthetic_triangles(600, seed=7)
+    m = S.model_from_triangles(xyz9)
+    packed = [tuple(np.float32(v) for v in xyz9[t, 3 * c:3 * c + 3]) for t in range(600) for c in range(3)]
+    tris = [(3 * t, 3 * t + 1, 3 * t + 2, 0) for t in range(600)]
+    nodes, prims, depth = R.build_bvh(packed, tris)
+    mats = [{"Kd": (np.float32(0.8),) * 3, "Ks": (np.float32(0),) * 3, "Ns": np.float32(10), "tex": None}]
+    _compare_scene(S.Scene.from_models([m]), R.flatten([(packed, nodes, prims, mats)]))
+    assert m.info()["max_depth"] == depth
+
+
+def test_glibc_rand_stream():
+    want = [1804289383, 846930886, 1681692777, 1714636915, 1957747793]  # glibc rand(), seed 1
+    assert S.glibc_rand(5).tolist() == want
+    g = R.GlibcRand()
+    assert [g() for _ in range(2000)] == S.glibc_rand(2000).tolist()
+    assert float(np.float32(want[0]) / np.float32(2147483648.0)) == pytest.approx(0.840187728, abs=1e-9)
+
+
+def test_glibc_rand_matches_libc():
+    import ctypes
+    import ctypes.util
+
+    libc = ctypes.CDLL(ctypes.util.find_library("c"))
+    libc.srand(1)
+    assert [libc.rand() for _ in range(1000)] == S.glibc_rand(1000).tolist()
+
+
+@pytest.mark.parametrize("gcc_order", [True, False])
+def test_noise_matches_restatement(gcc_order):
+    noise, noise_u = S.generate_noise(13, 11, gcc_order=gcc_order)
+    rn, ru = R.generate_noise(13 * 11, gcc_order=gcc_order)
+    assert noise.tobytes() == rn.tobytes() and noise_u.tobytes() == ru.tobytes()
+    norms = np.linalg.norm(noise.astype(np.float64), axis=1)
+    assert np.all(np.abs(norms - 1) < 1e-6) and np.all((noise_u >= 0) & (noise_u <= 1))
+
+
+def test_camera_basis():
+    cam = S.Camera(show_model=True)
+    assert cam.position.tolist() == [0.0, 9.0, 40.0]
+    f, u, r = R.camera_basis(-90.0, 0.0)
+    assert cam.front.tobytes() == np.array(f, np.float32).tobytes()
+    assert cam.up.tobytes() == np.array(u, np.float32).tobytes()
+    assert cam.right.tobytes() == np.array(r, np.float32).tobytes()
+    assert S.Camera(show_model=False).position.tolist() == [0.0, 1.0, 4.0]
+    cam.Rotate(30.0, -20.0)
+    f, u, r = R.camera_basis(-60.0, -20.0)
+    assert cam.front.tobytes() == np.array(f, np.float32).tobytes()
+
+
+def test_camera_height_rounding():
+    """GetCamera's int(width / aspect) (raytrace_compute.glsl:50): 1080 survives."""
+    for w, h in ((1920, 1080), (1000, 800), (4096, 4096), (256, 256), (1024, 1024)):
+        aspect = np.float32(w) / np.float32(h)
+        assert int(np.float32(w) / aspect) == h
+
+
+def _write_png(path, w, h, pixels, ctype=2):
+    import struct
+    import zlib
+
+    ch = {0: 1, 2: 3, 6: 4}[ctype]
+    raw = b"".join(b"\x00" + bytes(pixels[y * w * ch:(y + 1) * w * ch]) for y in range(h))
+
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xFFFFFFFF)
+
+    path.write_bytes(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, ctype, 0, 0, 0))
+                     + chunk(b"IDAT", zlib.compress(raw)) + chunk(b"IEND", b""))
+
+
+def test_texture_corner_albedo(tmp_path):
+    """texture(sampler2D, uv=(0,0)) with GL_REPEAT + GL_LINEAR = mean of the four corner texels."""
+    w, h = 5, 4
+    px = [0] * (w * h * 3)
+
+    def put(x, y, rgb):
+        px[(y * w + x) * 3:(y * w + x) * 3 + 3] = rgb
+
+    put(0, 0, (255, 0, 0)); put(w - 1, 0, (0, 255, 0)); put(0, h - 1, (0, 0, 255)); put(w - 1, h - 1, (255, 255, 255))
+    _write_png(tmp_path / "t.png", w, h, px)
+    (tmp_path / "m.mtl").write_text("newmtl tex\nKd 1 1 1\nNs 30\nmap_Kd t.png\n")
+    (tmp_path / "m.obj").write_text("mtllib m.mtl\nv 0 0 0\nv 1 0 0\nv 0 1 0\nusemtl tex\nf 1 2 3\n")
+    sc = S.Scene.from_models([S.load_obj(tmp_path / "m.obj")])
+    assert sc.mats[0]["use_texture"] == 1
+    np.testing.assert_allclose(sc.tex_albedo[0], [0.5, 0.5, 0.5], atol=1e-7)
+
+
+def test_missing_obj_raises(tmp_path):
+    with pytest.raises(S.SrtError):
+        S.load_obj(tmp_path / "nope.obj")
