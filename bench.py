@@ -43,17 +43,19 @@ def parse():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--max-depth", type=int, default=5)
     ap.add_argument("--synthetic-tris", type=int, default=10_000_000)
-    ap.add_argument("--band-rows", type=int, default=16)
+    ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
 
-def algorithmic_bytes(st: dict, pixels: int) -> int:
-    """32 B/node, 40 B/triangle test, 48 B/material, 4 B/uniform-noise fetch,
-    8 B/jitter fetch, 32 B/light record, plus the accumulation RMW (32 B) + RGBA8 store (4 B) per pixel."""
+def algorithmic_bytes(st: dict) -> int:
+    """Bytes one sample_kernel launch must move (SURVEY.md 8d per-unit prices): 32 B per node box test,
+    40 B per triangle test, 48 B per mesh-material fetch, 4 B per uniform-noise fetch, 8 B per jitter
+    fetch, 32 B per light record, and the 16-B radiance store per sample (the sample buffer that
+    accumulate_kernel sums; it replaces the reference's per-frame 32-B accumulation RMW)."""
     return (32 * st["nodes"] + 40 * st["tris"] + 48 * st["mat_reads"] + 4 * st["rng_u"] + 8 * st["rng_sq"]
-            + 32 * st["light_reads"] + 36 * pixels)
+            + 32 * st["light_reads"] + 16 * st["samples"])
 
 
 def cpu_baseline(setup, spp_first: int, target_s: float) -> dict:
@@ -136,15 +138,14 @@ def main():
     rdr = R.Renderer(setup, device=local_rank, stream=stream.cuda_stream, rank=rank, nranks=world,
                      band_rows=args.band_rows)
     c = rdr.compute
-    nbands = (H + args.band_rows - 1) // args.band_rows
-    rows_pad = ((nbands + world - 1) // world) * args.band_rows
+    from srt_amd import parallel as PAR
+
+    rows_pad = PAR.rows_pad(H, args.band_rows, world)
     local_rows = c.local_rows()
     accum_local = torch.zeros((rows_pad, W, 4), dtype=torch.float32, device=dev)
     out_local = torch.zeros((rows_pad, W), dtype=torch.int32, device=dev)
     c.set_image_buffers(accum_local.data_ptr(), out_local.data_ptr())
     if rank == 0 and world > 1:
-        gathered = [torch.empty_like(accum_local) for _ in range(world)]
-        gathered_flat = torch.empty((world, rows_pad, W, 4), dtype=torch.float32, device=dev)
         full_accum = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
         full_out = torch.empty((H, W), dtype=torch.int32, device=dev)
 
@@ -157,26 +158,19 @@ def main():
     if world > 1:
         dist.all_reduce(counts)
     total_rays = float(counts[0].item())
-    local_bytes = algorithmic_bytes(st, W * local_rows)
+    local_bytes = algorithmic_bytes(st)
 
-    ev_start = torch.cuda.Event(enable_timing=True)
-    ev_end = torch.cuda.Event(enable_timing=True)
     kernel_ms = []
 
     def step(timed: bool):
         rdr.clear()
-        if timed:
-            ev_start.record(stream)
         c.render_frames(2, spp, write_output=(world == 1), count=False)
-        if timed:
-            ev_end.record(stream)
         rdr.accum_frames = spp + 1
-        if world > 1:
-            dist.gather(accum_local, gathered if rank == 0 else None, dst=0)
+        if world > 1:  # the one exchange: every rank's radiance rows to rank 0 (RCCL over xGMI)
+            stacked = PAR.gather_bands(accum_local, dst=0)
             if rank == 0:
-                torch.stack(gathered, out=gathered_flat)
-                c.assemble_bands(gathered_flat.data_ptr(), world, rows_pad, args.band_rows, spp + 1, full_accum.data_ptr(),
-                                 full_out.data_ptr())
+                c.assemble_bands(stacked.data_ptr(), world, rows_pad, args.band_rows, spp + 1,
+                                 full_accum.data_ptr(), full_out.data_ptr())
 
     for _ in range(args.warmup):
         step(False)
@@ -188,7 +182,7 @@ def main():
     for _ in range(args.steps):
         step(True)
         torch.cuda.synchronize()
-        kernel_ms.append(ev_start.elapsed_time(ev_end))
+        kernel_ms.append(c.last_kernel_ms())  # HIP events around sample_kernel on the launch stream
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -235,7 +229,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
-                "kernel": "pathtrace_kernel<false>",
+                "kernel": "srt::sample_kernel<false, LDS, BLOCK> (HIP-event time per launch)",
                 "kernel_ms": round(k_ms, 3),
                 "algorithmic_bytes_per_launch": int(local_bytes),
             },

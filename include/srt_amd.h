@@ -99,6 +99,9 @@ int srt_finish(srt_context* ctx);
  * launches (count != 0) also fill srt_get_stats. */
 int srt_render_frames(srt_context* ctx, int frame_first, int nframes, int write_output, int count);
 int srt_get_stats(srt_context* ctx, srt_stats* out);
+/* Device time of the path-tracing kernel launches of the last render call
+ * (HIP events on the context's stream around each sample_kernel launch). */
+int srt_last_kernel_ms(srt_context* ctx, float* ms);
 int srt_reset_stats(srt_context* ctx);
 
 /* Row-band sharding for multi-GPU: this context owns bands b of `band_rows`

@@ -1154,6 +1154,9 @@ struct srt_context {
   // stats
   unsigned long long* d_stats = nullptr;
   srt_stats stats{};
+  // per-chunk HIP events around the sample kernel of the last render call
+  std::vector<hipEvent_t> ev;
+  int ev_used = 0;
 };
 
 namespace {
@@ -1341,17 +1344,27 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   kp.trav_frac16 = c->trav_frac16;
   if (count) HIP_OK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_N, c->stream));
   const int out_frames = kp.frame_first + kp.nframes - 1;
+  const int nchunks = (kp.nframes + chunk - 1) / chunk;
+  while ((int)c->ev.size() < 2 * nchunks) {
+    hipEvent_t e;
+    HIP_OK(hipEventCreate(&e));
+    c->ev.push_back(e);
+  }
+  c->ev_used = 0;
   for (int f0 = 0; f0 < kp.nframes; f0 += chunk) {
     srt::KParams kc = kp;
     kc.frame_first = kp.frame_first + f0;
     kc.nframes = std::min(chunk, kp.nframes - f0);
     kc.write_output = (f0 + chunk >= kp.nframes) ? kp.write_output : 0;
     int rc;
+    HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
     if (count && ldsm) rc = block == 512 ? LaunchSamples<true, true, 512>(c, kc, lds) : LaunchSamples<true, true, 1024>(c, kc, lds);
     else if (count) rc = LaunchSamples<true, false, 256>(c, kc, lds);
     else if (ldsm) rc = block == 512 ? LaunchSamples<false, true, 512>(c, kc, lds) : LaunchSamples<false, true, 1024>(c, kc, lds);
     else rc = LaunchSamples<false, false, 256>(c, kc, lds);
     if (rc) return rc;
+    HIP_OK(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
+    c->ev_used += 2;
     hipLaunchKernelGGL(srt::accumulate_kernel, pgrid, dim3(256), 0, c->stream, kc, out_frames);
     HIP_OK(hipGetLastError());
   }
@@ -1462,6 +1475,7 @@ int srt_destroy(srt_context* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   FreeDev(c->d_nodes); FreeDev(c->d_tris); FreeDev(c->d_mats); FreeDev(c->d_bvhs); FreeDev(c->d_lights);
   FreeDev(c->d_noise_xy); FreeDev(c->d_noise_u); FreeDev(c->d_stats); FreeDev(c->d_lbuf);
+  for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (!c->images_external) { FreeDev(c->d_accum); FreeDev(c->d_out); }
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1567,6 +1581,18 @@ int srt_render_frames(srt_context* c, int frame_first, int nframes, int write_ou
 int srt_finish(srt_context* c) {
   if (!c) return SRT_ERR_INVALID;
   HIP_OK(hipStreamSynchronize(c->stream));
+  return SRT_OK;
+}
+
+int srt_last_kernel_ms(srt_context* c, float* ms) {
+  if (!c || !ms) return SRT_ERR_INVALID;
+  *ms = 0.0f;
+  for (int i = 0; i + 1 < c->ev_used; i += 2) {
+    HIP_OK(hipEventSynchronize(c->ev[i + 1]));
+    float t = 0.0f;
+    HIP_OK(hipEventElapsedTime(&t, c->ev[i], c->ev[i + 1]));
+    *ms += t;
+  }
   return SRT_OK;
 }
 

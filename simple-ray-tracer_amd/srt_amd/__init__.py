@@ -371,6 +371,12 @@ class Compute:
         check(lib().srt_get_stats(self.ctx, C.byref(s)), "stats")
         return s.as_dict()
 
+    def last_kernel_ms(self) -> float:
+        """Device time of the sample-kernel launches of the last render (HIP events on the launch stream)."""
+        ms = C.c_float()
+        check(lib().srt_last_kernel_ms(self.ctx, C.byref(ms)), "last_kernel_ms")
+        return float(ms.value)
+
     def reset_stats(self):
         check(lib().srt_reset_stats(self.ctx), "reset_stats")
 

@@ -85,6 +85,7 @@ _SIGS = {
     "srt_finish": (C.c_int, [P]),
     "srt_render_frames": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int]),
     "srt_get_stats": (C.c_int, [P, C.POINTER(Stats)]),
+    "srt_last_kernel_ms": (C.c_int, [P, C.POINTER(C.c_float)]),
     "srt_reset_stats": (C.c_int, [P]),
     "srt_set_tiling": (C.c_int, [P, C.c_int, C.c_int, C.c_int]),
     "srt_local_rows": (C.c_int, [P]),
