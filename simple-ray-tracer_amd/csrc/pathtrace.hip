@@ -72,7 +72,16 @@ struct KParams {
 // Dynamic LDS of the path-tracing kernels: [scene copy (LDS mode)] [per-lane stacks].
 extern __shared__ __attribute__((aligned(16))) float4 g_smem[];
 
-enum { ST_RAYS = 0, ST_NODES, ST_TRIS, ST_RNGU, ST_RNGSQ, ST_LIGHTS, ST_MATS, ST_SAMPLES, ST_OVERFLOW, ST_MAXSTACK, ST_N };
+enum { ST_RAYS = 0, ST_NODES, ST_TRIS, ST_RNGU, ST_RNGSQ, ST_LIGHTS, ST_MATS, ST_SAMPLES, ST_OVERFLOW, ST_MAXSTACK,
+       ST_N, ST_CYC_REFILL = ST_N, ST_CYC_TRAV, ST_CYC_SHADE, ST_CYC_ITERS, ST_TOTAL };
+
+// Diagnostic build only (-DSRT_PHASE_TIMING): per-wave shader-clock stamps at the
+// phase boundaries of sample_kernel, summed into stats[ST_CYC_*].
+#ifdef SRT_PHASE_TIMING
+#define PHASE_STAMP(var) unsigned long long var = __builtin_amdgcn_s_memtime()
+#else
+#define PHASE_STAMP(var)
+#endif
 
 struct Counters {
   uint32_t v[ST_N];
@@ -199,62 +208,18 @@ __device__ __forceinline__ float box_t(f3 o, f3 inv, float4 lo, float4 hi) {
 
 __device__ __forceinline__ bool box_ok(float b, float dist) { return b < dist && !isinf_f(b); }
 
-// IntersectsTriangle (ray_intersects.glsl:61-96), Moller-Trumbore with edges
-// precomputed at upload.  The reference divides f = 1 / a per test; here an
-// approximate reciprocal (v_rcp_f32, 1 ulp) first REJECTS the triangles whose
-// u / v / u+v / t tests provably fail (margins of 2^-16 relative, far above the
-// <= 2^-21 combined rounding of the exact and approximate products); every
-// triangle not rejected that way is evaluated with the exact, correctly rounded
-// reference arithmetic, so the accept decision and t are bit-identical.
-__device__ __forceinline__ bool tri_test_exact(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& dist) {
-  const f3 h = cross(d, e2);
-  const float a = dot(e1, h);
-  if (a > -0.0001f && a < 0.0001f) return false;
-  const float f = 1.0f / a;
-  const f3 s = o - v0;
-  const float u = f * dot(s, h);
-  if (u < 0.0f || u > 1.0f) return false;
-  const f3 q = cross(s, e1);
-  const float v = f * dot(d, q);
-  if (v < 0.0f || u + v > 1.0f) return false;
-  const float t = f * dot(e2, q);
-  if (t > 0.00001f && t < dist) {
-    dist = t;
-    return true;
-  }
-  return false;
+// LDS byte offsets are 32-bit: keep the address arithmetic in 32 bits.
+__device__ __forceinline__ float4 lds4(uint32_t byte_off) {
+  return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(g_smem) + byte_off);
 }
-
-__device__ __forceinline__ bool tri_test(f3 o, f3 d, float4 A, float4 B, float4 C, float& dist) {
-  const f3 v0 = mk(A.x, A.y, A.z), e1 = mk(A.w, B.x, B.y), e2 = mk(B.z, B.w, C.x);
-  // every predicate below is evaluated without branching; only triangles
-  // that survive all conservative rejections take the exact path
-  const f3 h = cross(d, e2);
-  const float a = dot(e1, h);
-  const bool parallel = a > -0.0001f && a < 0.0001f;
-  const float r = __builtin_amdgcn_rcpf(a);
-  const f3 s = o - v0;
-  const float ua = r * dot(s, h);
-  const f3 q = cross(s, e1);
-  const float va = r * dot(d, q);
-  const float ta = r * dot(e2, q);
-  const bool in_range = __builtin_fabsf(a) < 1.0e30f;   // 1/a normal: the margins below hold
-  const bool reject = parallel |
-                      (in_range & ((ua < -1.0e-30f) | (ua > 1.0000153f) | (va < -1.0e-30f) |
-                                   (ua + va > 1.0f + 0.0000153f * __builtin_fmaxf(1.0f, va)) |
-                                   (ta < 0.0000099998f) | (ta > dist * 1.0000153f)));
-  if (reject) return false;
-  return tri_test_exact(o, d, v0, e1, e2, dist);
-}
-
 template <bool LDSM>
 __device__ __forceinline__ float4 node4(const KParams& kp, uint32_t i) {
-  if constexpr (LDSM) return g_smem[i];
+  if constexpr (LDSM) return lds4(i << 4);
   else return kp.nodes[i];
 }
 template <bool LDSM>
 __device__ __forceinline__ float4 tri4(const KParams& kp, uint32_t i) {
-  if constexpr (LDSM) return g_smem[(uint32_t)kp.nodes_f4 + i];
+  if constexpr (LDSM) return lds4(((uint32_t)kp.nodes_f4 + i) << 4);
   else return kp.tris[i];
 }
 
@@ -288,6 +253,26 @@ __device__ __forceinline__ void stk_ref(const Lane& ln, int sp, uint32_t& ref, u
   }
 }
 
+// IntersectsTriangle (ray_intersects.glsl:61-96, Moller-Trumbore with edges
+// precomputed at upload) evaluated without branches: every quantity the reference
+// computes on its way to each early return is computed, and the accept
+// predicate is their conjunction -- the same decision and the same t
+// (f = 1 / a is the correctly rounded division of the reference).
+__device__ __forceinline__ bool tri_accept(f3 o, f3 d, float4 A, float4 B, float4 C, float dist, float& tout) {
+  const f3 v0 = mk(A.x, A.y, A.z), e1 = mk(A.w, B.x, B.y), e2 = mk(B.z, B.w, C.x);
+  const f3 h = cross(d, e2);
+  const float a = dot(e1, h);
+  const bool parallel = (a > -0.0001f) & (a < 0.0001f);
+  const float f = 1.0f / a;
+  const f3 s = o - v0;
+  const float u = f * dot(s, h);
+  const f3 q = cross(s, e1);
+  const float v = f * dot(d, q);
+  const float t = f * dot(e2, q);
+  tout = t;
+  return !parallel & !((u < 0.0f) | (u > 1.0f)) & !((v < 0.0f) | (u + v > 1.0f)) & (t > 0.00001f) & (t < dist);
+}
+
 // Depth-first traversal in the reference's pop order (right child first).
 // Each child's box is tested once, when its parent is expanded; a child that
 // fails is never pushed (the running distance only shrinks, so it would fail
@@ -316,7 +301,9 @@ __device__ uint32_t traverse(const KParams& kp, const Lane& ln, Counters& c, uin
       // leaf: one triangle per step, in the reference's order
       bump<COUNT>(c, ST_TRIS);
       const uint32_t t3 = 3 * ref;
-      if (tri_test(o, d, tri4<LDSM>(kp, t3), tri4<LDSM>(kp, t3 + 1), tri4<LDSM>(kp, t3 + 2), dist)) {
+      float tt;
+      if (tri_accept(o, d, tri4<LDSM>(kp, t3), tri4<LDSM>(kp, t3 + 1), tri4<LDSM>(kp, t3 + 2), dist, tt)) {
+        dist = tt;
         hit = ref;
         if (any) break;
       }
@@ -624,36 +611,43 @@ struct Trav {
 
 constexpr uint32_t kNoneRef = 0xFFFFFFFFu;
 
-// One traversal step (see traverse() for the order argument).  `ro`/`rd` are
-// the world-space ray, `any` selects the shadow-ray (first hit) variant.
+// Sets up BVH `t.bi` for the world ray (the reference's per-model transform,
+// raytrace_compute.glsl:146-147) and tests its root box.
+template <bool COUNT, bool LDSM>
+__device__ __forceinline__ void trav_begin_bvh(const KParams& kp, Counters& c, Trav& t, f3 ro, f3 rd) {
+  const srt_bvh_record& b = kp.bvhs[t.bi];
+  t.o = xform(b.frame, ro, 1.0f);
+  t.d = xform(b.frame, rd, 0.0f);
+  t.inv = mk(1.0f / t.d.x, 1.0f / t.d.y, 1.0f / t.d.z);
+  const uint32_t root = b.first_index;
+  const float4 rlo = node4<LDSM>(kp, 2 * root + 2), rhi = node4<LDSM>(kp, 2 * root + 3);
+  bump<COUNT>(c, ST_NODES);
+  const bool ok = box_ok(box_t(t.o, t.inv, rlo, rhi), t.dist);
+  t.ref = ok ? __float_as_uint(rlo.w) : kNoneRef;
+  t.cnt = ok ? __float_as_uint(rhi.w) : 0u;
+  t.sp = 0;
+  t.start = false;
+}
+
+// One traversal step (see traverse() for the order argument): test one
+// triangle of the current leaf, or expand the current internal node; then
+// pop if nothing is current.  `any` selects the shadow-ray (first hit) variant.
 template <bool COUNT, bool LDSM>
 __device__ __forceinline__ void trav_step(const KParams& kp, const Lane& ln, Counters& c, Trav& t, f3 ro, f3 rd,
                                           bool any) {
-  if (t.start) {
-    const srt_bvh_record& b = kp.bvhs[t.bi];
-    t.o = xform(b.frame, ro, 1.0f);
-    t.d = xform(b.frame, rd, 0.0f);
-    t.inv = mk(1.0f / t.d.x, 1.0f / t.d.y, 1.0f / t.d.z);
-    const uint32_t root = b.first_index;
-    const float4 rlo = node4<LDSM>(kp, 2 * root + 2), rhi = node4<LDSM>(kp, 2 * root + 3);
-    bump<COUNT>(c, ST_NODES);
-    const bool ok = box_ok(box_t(t.o, t.inv, rlo, rhi), t.dist);
-    t.ref = ok ? __float_as_uint(rlo.w) : kNoneRef;
-    t.cnt = ok ? __float_as_uint(rhi.w) : 0u;
-    t.sp = 0;
-    t.start = false;
-  } else if (t.cnt > 0) {
+  if (t.start) trav_begin_bvh<COUNT, LDSM>(kp, c, t, ro, rd);  // only for BVHs after the first
+  if (t.cnt > 0) {
     bump<COUNT>(c, ST_TRIS);
     const uint32_t t3 = 3 * t.ref;
-    if (tri_test(t.o, t.d, tri4<LDSM>(kp, t3), tri4<LDSM>(kp, t3 + 1), tri4<LDSM>(kp, t3 + 2), t.dist)) {
-      t.hit = t.ref;
-      if (any) {
-        t.active = false;
-        return;
-      }
-    }
+    float tt;
+    const bool acc = tri_accept(t.o, t.d, tri4<LDSM>(kp, t3), tri4<LDSM>(kp, t3 + 1), tri4<LDSM>(kp, t3 + 2), t.dist, tt);
+    t.dist = acc ? tt : t.dist;
+    t.hit = acc ? t.ref : t.hit;
+    t.active = !(acc & any);
     ++t.ref;
-    if (--t.cnt == 0) t.ref = kNoneRef;
+    --t.cnt;
+    t.ref = (t.cnt == 0 || (acc & any)) ? kNoneRef : t.ref;
+    t.cnt = (acc & any) ? 0u : t.cnt;
   } else if (t.ref != kNoneRef) {
     const uint32_t pi = 2 * t.ref + 2;
     const float4 l0 = node4<LDSM>(kp, pi), h0 = node4<LDSM>(kp, pi + 1);
@@ -663,25 +657,24 @@ __device__ __forceinline__ void trav_step(const KParams& kp, const Lane& ln, Cou
     const float b1 = box_t(t.o, t.inv, l1, h1);
     const bool v0 = box_ok(b0, t.dist), v1 = box_ok(b1, t.dist);
     const uint32_t r0 = __float_as_uint(l0.w), n0 = __float_as_uint(h0.w);
-    if (v0 & v1) {
-      if (t.sp >= kp.stack_entries) {  // cannot happen for a validated BVH
-        bump<COUNT>(c, ST_OVERFLOW);
-        t.active = false;
-        return;
-      }
-      stk_push<LDSM>(ln, t.sp, r0, n0, b0);
-      ++t.sp;
-      if constexpr (COUNT) {
-        if ((uint32_t)t.sp > c.v[ST_MAXSTACK]) c.v[ST_MAXSTACK] = (uint32_t)t.sp;
-      }
+    // push c0 when both children pass; the slot is written unconditionally (it
+    // is free either way; the stack holds depth + 1 entries, validated at upload)
+    stk_push<LDSM>(ln, t.sp, r0, n0, b0);
+    t.sp += (v0 & v1) ? 1 : 0;
+    if constexpr (COUNT) {
+      if ((uint32_t)t.sp > c.v[ST_MAXSTACK]) c.v[ST_MAXSTACK] = (uint32_t)t.sp;
     }
     t.ref = v1 ? __float_as_uint(l1.w) : (v0 ? r0 : kNoneRef);
     t.cnt = v1 ? __float_as_uint(h1.w) : (v0 ? n0 : 0u);
   }
-  if (t.cnt == 0 && t.ref == kNoneRef) {
+  if (t.active & (t.cnt == 0) & (t.ref == kNoneRef)) {
     if (t.sp > 0) {
       --t.sp;
-      if (stk_t<LDSM>(ln, t.sp) < t.dist) stk_ref<LDSM>(ln, t.sp, t.ref, t.cnt);
+      const bool take = stk_t<LDSM>(ln, t.sp) < t.dist;
+      uint32_t r, n;
+      stk_ref<LDSM>(ln, t.sp, r, n);
+      t.ref = take ? r : kNoneRef;
+      t.cnt = take ? n : 0u;
     } else if ((any && t.hit != kNoneRef) || t.bi + 1 >= kp.bvh_count) {
       t.active = false;  // CheckHit's loop over bvh_count is complete
     } else {
@@ -738,9 +731,15 @@ __global__ __launch_bounds__(BLOCK) void sample_kernel(KParams kp) {
     tr.hit = kNoneRef;
     tr.bi = 0;
     tr.active = true;
-    tr.start = true;
+    tr.start = false;
     bump<COUNT>(c, ST_RAYS);
-    if (!kp.show_model) {  // the five spheres are "traversed" in one go
+    if (kp.show_model) {
+      trav_begin_bvh<COUNT, LDSM>(kp, c, tr, ro, rd);
+      if (tr.cnt == 0 && tr.ref == kNoneRef) {  // root box missed: next BVH, or done
+        if (kp.bvh_count > 1) tr.start = true, tr.bi = 1;
+        else tr.active = false;
+      }
+    } else {  // the five spheres are "traversed" in one go
       float dist = tmax;
       hit_sphere = trace_spheres(ro, rd, 0.001f, dist, shadow_phase);
       tr.dist = dist;
@@ -753,7 +752,11 @@ __global__ __launch_bounds__(BLOCK) void sample_kernel(KParams kp) {
     has_work = false;
   };
 
+#ifdef SRT_PHASE_TIMING
+  unsigned long long cyc_refill = 0, cyc_trav = 0, cyc_shade = 0, iters = 0;
+#endif
   for (;;) {
+    PHASE_STAMP(t_a);
     // ---- (A) idle lanes take the next items of the wave's batches ----
     for (;;) {
       const unsigned long long idle = __ballot(!has_work);
@@ -807,6 +810,7 @@ __global__ __launch_bounds__(BLOCK) void sample_kernel(KParams kp) {
       }
     }
     if (__ballot(has_work) == 0ull) break;
+    PHASE_STAMP(t_b);
 
     // ---- (B) traverse until too few lanes are still traversing ----
     if (kp.show_model) {
@@ -820,6 +824,7 @@ __global__ __launch_bounds__(BLOCK) void sample_kernel(KParams kp) {
       }
     }
 
+    PHASE_STAMP(t_c);
     // ---- (C) lanes whose ray returned: shade (GetRayColor's loop body) ----
     if (has_work && !tr.active) {
       const bool hit = kp.show_model ? (tr.hit != kNoneRef) : (hit_sphere >= 0);
@@ -986,7 +991,22 @@ __global__ __launch_bounds__(BLOCK) void sample_kernel(KParams kp) {
         }
       }
     }
+#ifdef SRT_PHASE_TIMING
+    PHASE_STAMP(t_d);
+    cyc_refill += t_b - t_a;
+    cyc_trav += t_c - t_b;
+    cyc_shade += t_d - t_c;
+    ++iters;
+#endif
   }
+#ifdef SRT_PHASE_TIMING
+  if (lane == 0) {
+    atomicAdd(&kp.stats[ST_CYC_REFILL], cyc_refill);
+    atomicAdd(&kp.stats[ST_CYC_TRAV], cyc_trav);
+    atomicAdd(&kp.stats[ST_CYC_SHADE], cyc_shade);
+    atomicAdd(&kp.stats[ST_CYC_ITERS], iters);
+  }
+#endif
   flush_counters<COUNT>(kp, c);
 }
 
@@ -1342,7 +1362,7 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   }
   kp.lbuf = c->d_lbuf;
   kp.trav_frac16 = c->trav_frac16;
-  if (count) HIP_OK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_N, c->stream));
+  HIP_OK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_TOTAL, c->stream));
   const int out_frames = kp.frame_first + kp.nframes - 1;
   const int nchunks = (kp.nframes + chunk - 1) / chunk;
   while ((int)c->ev.size() < 2 * nchunks) {
@@ -1459,7 +1479,7 @@ int srt_create(int device, void* stream, srt_context** out) {
     }
     c->own_stream = true;
   }
-  if (hipMalloc(&c->d_stats, sizeof(unsigned long long) * srt::ST_N) != hipSuccess) {
+  if (hipMalloc(&c->d_stats, sizeof(unsigned long long) * srt::ST_TOTAL) != hipSuccess) {
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
     srt::SetError("hipMalloc(stats) failed");
@@ -1580,6 +1600,15 @@ int srt_render_frames(srt_context* c, int frame_first, int nframes, int write_ou
 
 int srt_finish(srt_context* c) {
   if (!c) return SRT_ERR_INVALID;
+  HIP_OK(hipStreamSynchronize(c->stream));
+  return SRT_OK;
+}
+
+// Diagnostic: shader-clock cycles per phase of the last render (SRT_PHASE_TIMING builds only; zeros otherwise).
+extern "C" int srt_debug_phase_cycles(srt_context* c, unsigned long long out[4]) {
+  if (!c || !out) return SRT_ERR_INVALID;
+  HIP_OK(hipMemcpyAsync(out, c->d_stats + srt::ST_CYC_REFILL, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                        c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
   return SRT_OK;
 }

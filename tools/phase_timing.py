@@ -1,0 +1,18 @@
+"""Diagnostic: phase split of sample_kernel (needs the SRT_PHASE_TIMING build via SRT_LIB_PATH)."""
+import ctypes as C, sys, pathlib, os
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd")); sys.path.insert(0, str(ROOT))
+import srt_amd as S
+from srt_amd import render as R, _lib
+spp = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+setup = R.make_setup(1920, 1080, show_model=True, models=[R.rubik_model(ROOT / "tests/golden/objects")])
+r = R.Renderer(setup)
+r.render(spp); r.finish()
+r.render(spp); r.finish()
+lib = _lib.lib(); lib.srt_debug_phase_cycles.argtypes = [C.c_void_p, C.c_void_p]
+import numpy as np
+out = np.zeros(4, np.uint64)
+lib.srt_debug_phase_cycles(r.compute.ctx, out.ctypes.data)
+tot = out[:3].sum()
+print("kernel_ms", r.compute.last_kernel_ms(), "refill %.1f%% trav %.1f%% shade %.1f%% iters/wave %.0f" % (
+    100 * out[0] / tot, 100 * out[1] / tot, 100 * out[2] / tot, out[3] / 4096))
