@@ -217,6 +217,13 @@ __device__ __forceinline__ float4 node4(const KParams& kp, uint32_t i) {
   if constexpr (LDSM) return lds4(i << 4);
   else return kp.nodes[i];
 }
+// the records of triangle `i` onwards (3 float4 per triangle)
+template <bool LDSM>
+__device__ __forceinline__ const float4* tri_ptr(const KParams& kp, uint32_t i) {
+  if constexpr (LDSM)
+    return reinterpret_cast<const float4*>(reinterpret_cast<const char*>(g_smem) + (((uint32_t)kp.nodes_f4 + 3 * i) << 4));
+  else return kp.tris + 3 * (size_t)i;
+}
 template <bool LDSM>
 __device__ __forceinline__ float4 tri4(const KParams& kp, uint32_t i) {
   if constexpr (LDSM) return lds4(((uint32_t)kp.nodes_f4 + i) << 4);
@@ -610,6 +617,12 @@ struct Trav {
 };
 
 constexpr uint32_t kNoneRef = 0xFFFFFFFFu;
+#ifndef SRT_LEAF_TRIS
+#define SRT_LEAF_TRIS 2
+#endif
+constexpr int kLeafTris = SRT_LEAF_TRIS;  // triangles tested per leaf step
+constexpr int kTriPad = 3;                // zero records past the triangle array (>= kLeafTris - 1)
+static_assert(kLeafTris >= 1 && kLeafTris - 1 <= kTriPad, "kLeafTris");
 
 // Sets up BVH `t.bi` for the world ray (the reference's per-model transform,
 // raytrace_compute.glsl:146-147) and tests its root box.
@@ -637,17 +650,31 @@ __device__ __forceinline__ void trav_step(const KParams& kp, const Lane& ln, Cou
                                           bool any) {
   if (t.start) trav_begin_bvh<COUNT, LDSM>(kp, c, t, ro, rd);  // only for BVHs after the first
   if (t.cnt > 0) {
-    bump<COUNT>(c, ST_TRIS);
-    const uint32_t t3 = 3 * t.ref;
-    float tt;
-    const bool acc = tri_accept(t.o, t.d, tri4<LDSM>(kp, t3), tri4<LDSM>(kp, t3 + 1), tri4<LDSM>(kp, t3 + 2), t.dist, tt);
-    t.dist = acc ? tt : t.dist;
-    t.hit = acc ? t.ref : t.hit;
-    t.active = !(acc & any);
-    ++t.ref;
-    --t.cnt;
-    t.ref = (t.cnt == 0 || (acc & any)) ? kNoneRef : t.ref;
-    t.cnt = (acc & any) ? 0u : t.cnt;
+    // up to kLeafTris triangles per step, in order: each is tested against the
+    // distance the previous one left; a shadow ray stops at its first accept
+    // (the triangle array is padded with kLeafTris - 1 zero records)
+    const uint32_t n = t.cnt < (uint32_t)kLeafTris ? t.cnt : (uint32_t)kLeafTris;
+    bump<COUNT>(c, ST_TRIS, n);
+    float dist = t.dist;
+    uint32_t hit = t.hit;
+    bool stop = false;
+    const float4* tp = tri_ptr<LDSM>(kp, t.ref);
+#pragma unroll
+    for (int k = 0; k < kLeafTris; ++k) {
+      float tk;
+      const bool tk_ok = tri_accept(t.o, t.d, tp[3 * k], tp[3 * k + 1], tp[3 * k + 2], dist, tk);
+      const bool ak = k == 0 ? tk_ok : (((uint32_t)k < n) & !stop & tk_ok);  // a leaf holds >= 1 triangle
+      dist = ak ? tk : dist;
+      hit = ak ? t.ref + k : hit;
+      stop = stop | (ak & any);
+    }
+    t.dist = dist;
+    t.hit = hit;
+    t.ref += n;
+    t.cnt -= n;
+    t.active = !stop;
+    t.ref = (t.cnt == 0 || stop) ? kNoneRef : t.ref;
+    t.cnt = stop ? 0u : t.cnt;
   } else if (t.ref != kNoneRef) {
     const uint32_t pi = 2 * t.ref + 2;
     const float4 l0 = node4<LDSM>(kp, pi), h0 = node4<LDSM>(kp, pi + 1);
@@ -814,12 +841,13 @@ __global__ __launch_bounds__(BLOCK) void sample_kernel(KParams kp) {
 
     // ---- (B) traverse until too few lanes are still traversing ----
     if (kp.show_model) {
+      // has_work is fixed during traversal; trav_frac16 <= 16 makes
+      // n_trav * 16 < n_work * trav_frac16 imply n_trav < n_work
+      const int work_lim = __popcll(__ballot(has_work)) * kp.trav_frac16;
       for (;;) {
         const unsigned long long trav = __ballot(tr.active);
         if (trav == 0ull) break;
-        const int n_trav = __popcll(trav);
-        const int n_work = __popcll(__ballot(has_work));
-        if (n_trav < n_work && n_trav * 16 < n_work * kp.trav_frac16) break;
+        if (__popcll(trav) * 16 < work_lim) break;
         if (tr.active) trav_step<COUNT, LDSM>(kp, ln, c, tr, ro, rd, shadow_phase);
       }
     }
@@ -1168,7 +1196,7 @@ struct srt_context {
   float4* d_lbuf = nullptr;
   size_t lbuf_bytes = 0;
   size_t lbuf_cap = (size_t)16 << 30;  // SRT_SAMPLE_BUFFER_MB
-  int trav_frac16 = 10;                // SRT_TRAV_FRAC16 (measured best on Rubik 1080p: 8..10)
+  int trav_frac16 = 8;                 // SRT_TRAV_FRAC16 (measured best on Rubik 1080p with 2-triangle leaf steps)
   int lds_block = 1024;                // SRT_LDS_BLOCK (512 or 1024 threads per block in LDS mode)
   int num_cus = 256;
   // stats
@@ -1304,7 +1332,7 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
   kp->ext_h = c->H;
   kp->stack_entries = c->stack_entries;
   kp->nodes_f4 = (int)(2 * ((size_t)c->n_nodes + 1));
-  kp->tris_f4 = (int)(3 * (size_t)std::max<uint32_t>(c->n_tris, 1));
+  kp->tris_f4 = (int)(3 * ((size_t)c->n_tris + srt::kTriPad));  // with the padding records
   CameraParams(c, kp);
   return SRT_OK;
 }
@@ -1677,7 +1705,8 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
     hm[2 * (size_t)i + 1] = make_float4(m.specular[0], m.specular[1], m.specular[2], 0.0f);
   }
   // triangles: v0, e1 = v1 - v0, e2 = v2 - v0, material
-  std::vector<float4> ht(3 * (size_t)std::max<uint32_t>(n_tris, 1), make_float4(0, 0, 0, 0));
+  // kTriPad zero records past the end: a multi-triangle leaf step may read (and discard) them
+  std::vector<float4> ht(3 * ((size_t)n_tris + srt::kTriPad), make_float4(0, 0, 0, 0));
   auto vert = [&](uint32_t i, int k) -> float { return i < n_verts ? verts[i].vertex[k] : 0.0f; };
   for (uint32_t t = 0; t < n_tris; ++t) {
     const srt_triangle& tr = tris[t];
