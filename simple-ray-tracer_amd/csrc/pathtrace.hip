@@ -260,6 +260,20 @@ __device__ __forceinline__ void stk_ref(const Lane& ln, int sp, uint32_t& ref, u
   }
 }
 
+// 1.0f / a, correctly rounded, for every a that is not denormal.  v_rcp_f32
+// plus one FMA Newton step equals the correctly rounded quotient for every
+// 2^-126 <= |a| < 2^126 (all 2^32 inputs checked on gfx950:
+// tools/rcp_exhaustive.hip, tests/test_gpu_rcp.py); |a| >= 2^126, inf and NaN
+// take the full division on a branch that is skipped unless some lane of the
+// wave needs it.  Callers must not use the result for denormal a (the
+// triangle test rejects |a| < 1e-4 before f matters).
+__device__ __forceinline__ float recip_normal(float a) {
+  const float r = __builtin_amdgcn_rcpf(a);
+  float f = __builtin_fmaf(__builtin_fmaf(-a, r, 1.0f), r, r);
+  if (__builtin_expect(!(__builtin_fabsf(a) < 0x1p126f), 0)) f = 1.0f / a;
+  return f;
+}
+
 // IntersectsTriangle (ray_intersects.glsl:61-96, Moller-Trumbore with edges
 // precomputed at upload) evaluated without branches: every quantity the reference
 // computes on its way to each early return is computed, and the accept
@@ -270,7 +284,7 @@ __device__ __forceinline__ bool tri_accept(f3 o, f3 d, float4 A, float4 B, float
   const f3 h = cross(d, e2);
   const float a = dot(e1, h);
   const bool parallel = (a > -0.0001f) & (a < 0.0001f);
-  const float f = 1.0f / a;
+  const float f = recip_normal(a);  // |a| < 1e-4 is rejected (parallel)
   const f3 s = o - v0;
   const float u = f * dot(s, h);
   const f3 q = cross(s, e1);
