@@ -73,7 +73,9 @@ struct KParams {
 extern __shared__ __attribute__((aligned(16))) float4 g_smem[];
 
 enum { ST_RAYS = 0, ST_NODES, ST_TRIS, ST_RNGU, ST_RNGSQ, ST_LIGHTS, ST_MATS, ST_SAMPLES, ST_OVERFLOW, ST_MAXSTACK,
-       ST_N, ST_CYC_REFILL = ST_N, ST_CYC_TRAV, ST_CYC_SHADE, ST_CYC_ITERS, ST_TOTAL };
+       ST_N, ST_CYC_REFILL = ST_N, ST_CYC_TRAV, ST_CYC_SHADE, ST_CYC_ITERS,
+       // lane occupancy of the traversal loop (summed popcounts per iteration) and of shading
+       ST_DBG_TITERS, ST_DBG_WORK, ST_DBG_TRAV, ST_DBG_LEAF, ST_DBG_INT, ST_DBG_SHADE, ST_TOTAL };
 
 // Diagnostic build only (-DSRT_PHASE_TIMING): per-wave shader-clock stamps at the
 // phase boundaries of sample_kernel, summed into stats[ST_CYC_*].
@@ -635,6 +637,12 @@ constexpr uint32_t kNoneRef = 0xFFFFFFFFu;
 #define SRT_LEAF_TRIS 2
 #endif
 constexpr int kLeafTris = SRT_LEAF_TRIS;  // triangles tested per leaf step
+// Sub-steps of one traversal iteration: 'I' expands an internal node, 'L'
+// tests a leaf's next triangles; each is followed by a pop if nothing is current.
+#ifndef SRT_STEP_PATTERN
+#define SRT_STEP_PATTERN "ILILILIL"
+#endif
+constexpr char kStepPattern[] = SRT_STEP_PATTERN;
 constexpr int kTriPad = 3;                // zero records past the triangle array (>= kLeafTris - 1)
 static_assert(kLeafTris >= 1 && kLeafTris - 1 <= kTriPad, "kLeafTris");
 
@@ -656,59 +664,64 @@ __device__ __forceinline__ void trav_begin_bvh(const KParams& kp, Counters& c, T
   t.start = false;
 }
 
-// One traversal step (see traverse() for the order argument): test one
-// triangle of the current leaf, or expand the current internal node; then
-// pop if nothing is current.  `any` selects the shadow-ray (first hit) variant.
+// Leaf sub-step: up to kLeafTris triangles of the current leaf, in order: each
+// is tested against the distance the previous one left; a shadow ray stops at
+// its first accept (the triangle array is padded with kTriPad zero records).
 template <bool COUNT, bool LDSM>
-__device__ __forceinline__ void trav_step(const KParams& kp, const Lane& ln, Counters& c, Trav& t, f3 ro, f3 rd,
-                                          bool any) {
-  if (t.start) trav_begin_bvh<COUNT, LDSM>(kp, c, t, ro, rd);  // only for BVHs after the first
-  if (t.cnt > 0) {
-    // up to kLeafTris triangles per step, in order: each is tested against the
-    // distance the previous one left; a shadow ray stops at its first accept
-    // (the triangle array is padded with kLeafTris - 1 zero records)
-    const uint32_t n = t.cnt < (uint32_t)kLeafTris ? t.cnt : (uint32_t)kLeafTris;
-    bump<COUNT>(c, ST_TRIS, n);
-    float dist = t.dist;
-    uint32_t hit = t.hit;
-    bool stop = false;
-    const float4* tp = tri_ptr<LDSM>(kp, t.ref);
+__device__ __forceinline__ void trav_leaf(const KParams& kp, Counters& c, Trav& t, bool any) {
+  const uint32_t n = t.cnt < (uint32_t)kLeafTris ? t.cnt : (uint32_t)kLeafTris;
+  bump<COUNT>(c, ST_TRIS, n);
+  float dist = t.dist;
+  uint32_t hit = t.hit;
+  bool stop = false;
+  const float4* tp = tri_ptr<LDSM>(kp, t.ref);
 #pragma unroll
-    for (int k = 0; k < kLeafTris; ++k) {
-      float tk;
-      const bool tk_ok = tri_accept(t.o, t.d, tp[3 * k], tp[3 * k + 1], tp[3 * k + 2], dist, tk);
-      const bool ak = k == 0 ? tk_ok : (((uint32_t)k < n) & !stop & tk_ok);  // a leaf holds >= 1 triangle
-      dist = ak ? tk : dist;
-      hit = ak ? t.ref + k : hit;
-      stop = stop | (ak & any);
-    }
-    t.dist = dist;
-    t.hit = hit;
-    t.ref += n;
-    t.cnt -= n;
-    t.active = !stop;
-    t.ref = (t.cnt == 0 || stop) ? kNoneRef : t.ref;
-    t.cnt = stop ? 0u : t.cnt;
-  } else if (t.ref != kNoneRef) {
-    const uint32_t pi = 2 * t.ref + 2;
-    const float4 l0 = node4<LDSM>(kp, pi), h0 = node4<LDSM>(kp, pi + 1);
-    const float4 l1 = node4<LDSM>(kp, pi + 2), h1 = node4<LDSM>(kp, pi + 3);
-    bump<COUNT>(c, ST_NODES, 2);
-    const float b0 = box_t(t.o, t.inv, l0, h0);
-    const float b1 = box_t(t.o, t.inv, l1, h1);
-    const bool v0 = box_ok(b0, t.dist), v1 = box_ok(b1, t.dist);
-    const uint32_t r0 = __float_as_uint(l0.w), n0 = __float_as_uint(h0.w);
-    // push c0 when both children pass; the slot is written unconditionally (it
-    // is free either way; the stack holds depth + 1 entries, validated at upload)
-    stk_push<LDSM>(ln, t.sp, r0, n0, b0);
-    t.sp += (v0 & v1) ? 1 : 0;
-    if constexpr (COUNT) {
-      if ((uint32_t)t.sp > c.v[ST_MAXSTACK]) c.v[ST_MAXSTACK] = (uint32_t)t.sp;
-    }
-    t.ref = v1 ? __float_as_uint(l1.w) : (v0 ? r0 : kNoneRef);
-    t.cnt = v1 ? __float_as_uint(h1.w) : (v0 ? n0 : 0u);
+  for (int k = 0; k < kLeafTris; ++k) {
+    float tk;
+    const bool tk_ok = tri_accept(t.o, t.d, tp[3 * k], tp[3 * k + 1], tp[3 * k + 2], dist, tk);
+    const bool ak = k == 0 ? tk_ok : (((uint32_t)k < n) & !stop & tk_ok);  // a leaf holds >= 1 triangle
+    dist = ak ? tk : dist;
+    hit = ak ? t.ref + k : hit;
+    stop = stop | (ak & any);
   }
-  if (t.active & (t.cnt == 0) & (t.ref == kNoneRef)) {
+  t.dist = dist;
+  t.hit = hit;
+  t.ref += n;
+  t.cnt -= n;
+  t.active = !stop;
+  t.ref = (t.cnt == 0 || stop) ? kNoneRef : t.ref;
+  t.cnt = stop ? 0u : t.cnt;
+}
+
+// Internal sub-step: test both children's boxes; push c0 when both pass, go to
+// c1 if it passes, else to c0 if it passes.
+template <bool COUNT, bool LDSM>
+__device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln, Counters& c, Trav& t) {
+  const uint32_t pi = 2 * t.ref + 2;
+  const float4 l0 = node4<LDSM>(kp, pi), h0 = node4<LDSM>(kp, pi + 1);
+  const float4 l1 = node4<LDSM>(kp, pi + 2), h1 = node4<LDSM>(kp, pi + 3);
+  bump<COUNT>(c, ST_NODES, 2);
+  const float b0 = box_t(t.o, t.inv, l0, h0);
+  const float b1 = box_t(t.o, t.inv, l1, h1);
+  const bool v0 = box_ok(b0, t.dist), v1 = box_ok(b1, t.dist);
+  const uint32_t r0 = __float_as_uint(l0.w), n0 = __float_as_uint(h0.w);
+  // the c0 slot is written unconditionally (it is free either way; the stack
+  // holds depth + 1 entries, validated at upload)
+  stk_push<LDSM>(ln, t.sp, r0, n0, b0);
+  t.sp += (v0 & v1) ? 1 : 0;
+  if constexpr (COUNT) {
+    if ((uint32_t)t.sp > c.v[ST_MAXSTACK]) c.v[ST_MAXSTACK] = (uint32_t)t.sp;
+  }
+  t.ref = v1 ? __float_as_uint(l1.w) : (v0 ? r0 : kNoneRef);
+  t.cnt = v1 ? __float_as_uint(h1.w) : (v0 ? n0 : 0u);
+}
+
+// Nothing current: pop one entry (visited if it still beats the running
+// distance), or finish this BVH.  A lane whose next BVH is pending (`start`,
+// set up at the next iteration) does nothing.
+template <bool LDSM>
+__device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav& t, bool any) {
+  if (t.active & !t.start & (t.cnt == 0) & (t.ref == kNoneRef)) {
     if (t.sp > 0) {
       --t.sp;
       const bool take = stk_t<LDSM>(ln, t.sp) < t.dist;
@@ -723,6 +736,31 @@ __device__ __forceinline__ void trav_step(const KParams& kp, const Lane& ln, Cou
       t.start = true;
     }
   }
+}
+
+template <bool COUNT, bool LDSM, int K>
+__device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln, Counters& c, Trav& t, bool any) {
+  if constexpr (kStepPattern[K] != 0) {
+    if constexpr (kStepPattern[K] == 'I') {
+      if (t.cnt == 0 && t.ref != kNoneRef) trav_internal<COUNT, LDSM>(kp, ln, c, t);
+    } else {
+      if (t.cnt > 0) trav_leaf<COUNT, LDSM>(kp, c, t, any);
+    }
+    trav_pop<LDSM>(kp, ln, t, any);
+    trav_substeps<COUNT, LDSM, K + 1>(kp, ln, c, t, any);
+  }
+}
+
+// One traversal iteration (see traverse() for the order argument): the
+// sub-steps of kStepPattern in turn, each taken by the lanes whose current
+// node is of its kind, so a lane makes up to strlen(kStepPattern) steps of
+// its own sequence per iteration, in order.  `any` selects the shadow-ray
+// (first hit) variant.
+template <bool COUNT, bool LDSM>
+__device__ __forceinline__ void trav_step(const KParams& kp, const Lane& ln, Counters& c, Trav& t, f3 ro, f3 rd,
+                                          bool any) {
+  if (t.start) trav_begin_bvh<COUNT, LDSM>(kp, c, t, ro, rd);  // only for BVHs after the first
+  trav_substeps<COUNT, LDSM, 0>(kp, ln, c, t, any);
 }
 
 __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
@@ -795,6 +833,7 @@ __global__ __launch_bounds__(BLOCK) void sample_kernel(KParams kp) {
 
 #ifdef SRT_PHASE_TIMING
   unsigned long long cyc_refill = 0, cyc_trav = 0, cyc_shade = 0, iters = 0;
+  unsigned long long d_titers = 0, d_work = 0, d_trav = 0, d_leaf = 0, d_int = 0, d_shade = 0;
 #endif
   for (;;) {
     PHASE_STAMP(t_a);
@@ -862,11 +901,21 @@ __global__ __launch_bounds__(BLOCK) void sample_kernel(KParams kp) {
         const unsigned long long trav = __ballot(tr.active);
         if (trav == 0ull) break;
         if (__popcll(trav) * 16 < work_lim) break;
+#ifdef SRT_PHASE_TIMING
+        ++d_titers;
+        d_work += __popcll(__ballot(has_work));
+        d_trav += __popcll(trav);
+        d_leaf += __popcll(__ballot(tr.active && tr.cnt > 0));
+        d_int += __popcll(__ballot(tr.active && tr.cnt == 0 && tr.ref != kNoneRef));
+#endif
         if (tr.active) trav_step<COUNT, LDSM>(kp, ln, c, tr, ro, rd, shadow_phase);
       }
     }
 
     PHASE_STAMP(t_c);
+#ifdef SRT_PHASE_TIMING
+    d_shade += __popcll(__ballot(has_work && !tr.active));
+#endif
     // ---- (C) lanes whose ray returned: shade (GetRayColor's loop body) ----
     if (has_work && !tr.active) {
       const bool hit = kp.show_model ? (tr.hit != kNoneRef) : (hit_sphere >= 0);
@@ -1047,6 +1096,12 @@ __global__ __launch_bounds__(BLOCK) void sample_kernel(KParams kp) {
     atomicAdd(&kp.stats[ST_CYC_TRAV], cyc_trav);
     atomicAdd(&kp.stats[ST_CYC_SHADE], cyc_shade);
     atomicAdd(&kp.stats[ST_CYC_ITERS], iters);
+    atomicAdd(&kp.stats[ST_DBG_TITERS], d_titers);
+    atomicAdd(&kp.stats[ST_DBG_WORK], d_work);
+    atomicAdd(&kp.stats[ST_DBG_TRAV], d_trav);
+    atomicAdd(&kp.stats[ST_DBG_LEAF], d_leaf);
+    atomicAdd(&kp.stats[ST_DBG_INT], d_int);
+    atomicAdd(&kp.stats[ST_DBG_SHADE], d_shade);
   }
 #endif
   flush_counters<COUNT>(kp, c);
@@ -1647,9 +1702,12 @@ int srt_finish(srt_context* c) {
 }
 
 // Diagnostic: shader-clock cycles per phase of the last render (SRT_PHASE_TIMING builds only; zeros otherwise).
-extern "C" int srt_debug_phase_cycles(srt_context* c, unsigned long long out[4]) {
+// out[0..3]: refill / traversal / shading cycles, outer iterations; out[4..9]: traversal
+// iterations and summed lane counts (working, traversing, at a leaf, at an internal node),
+// lanes shading (summed over outer iterations).
+extern "C" int srt_debug_phase_cycles(srt_context* c, unsigned long long out[10]) {
   if (!c || !out) return SRT_ERR_INVALID;
-  HIP_OK(hipMemcpyAsync(out, c->d_stats + srt::ST_CYC_REFILL, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+  HIP_OK(hipMemcpyAsync(out, c->d_stats + srt::ST_CYC_REFILL, 10 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                         c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
   return SRT_OK;

@@ -11,8 +11,11 @@ r.render(spp); r.finish()
 r.render(spp); r.finish()
 lib = _lib.lib(); lib.srt_debug_phase_cycles.argtypes = [C.c_void_p, C.c_void_p]
 import numpy as np
-out = np.zeros(4, np.uint64)
+out = np.zeros(10, np.uint64)
 lib.srt_debug_phase_cycles(r.compute.ctx, out.ctypes.data)
 tot = out[:3].sum()
 print("kernel_ms", r.compute.last_kernel_ms(), "refill %.1f%% trav %.1f%% shade %.1f%% iters/wave %.0f" % (
     100 * out[0] / tot, 100 * out[1] / tot, 100 * out[2] / tot, out[3] / 4096))
+ti, wk, tv, lf, it, sh = (float(v) for v in out[4:10])
+print("trav iters/wave %.0f  per iteration: working %.1f traversing %.1f leaf %.1f internal %.1f pop-only %.1f lanes;"
+      " shading lanes/outer iter %.1f" % (ti / 4096, wk / ti, tv / ti, lf / ti, it / ti, (tv - lf - it) / ti, sh / float(out[3])))
