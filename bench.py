@@ -232,6 +232,10 @@ def main():
                 "kernel": "srt::sample_kernel<false, LDS, BLOCK> (HIP-event time per launch)",
                 "kernel_ms": round(k_ms, 3),
                 "algorithmic_bytes_per_launch": int(local_bytes),
+                "note": "SURVEY 8d bytes (node/triangle/material/noise/light reads) per launch / kernel time. "
+                        "The scene is read from its LDS copy and the noise from L2/MALL, so these bytes are not "
+                        "HBM traffic (measured HBM bytes: traffic) and frac > 1 means on-chip reuse. The kernel is "
+                        "bound by VALU issue under divergence (DESIGN.md section 5).",
             },
         }
         if world == 1 and not args.no_cpu_baseline:
