@@ -75,7 +75,22 @@ extern __shared__ __attribute__((aligned(16))) float4 g_smem[];
 enum { ST_RAYS = 0, ST_NODES, ST_TRIS, ST_RNGU, ST_RNGSQ, ST_LIGHTS, ST_MATS, ST_SAMPLES, ST_OVERFLOW, ST_MAXSTACK,
        ST_N, ST_CYC_REFILL = ST_N, ST_CYC_TRAV, ST_CYC_SHADE, ST_CYC_ITERS,
        // lane occupancy of the traversal loop (summed popcounts per iteration) and of shading
-       ST_DBG_TITERS, ST_DBG_WORK, ST_DBG_TRAV, ST_DBG_LEAF, ST_DBG_INT, ST_DBG_SHADE, ST_TOTAL };
+       ST_DBG_TITERS, ST_DBG_WORK, ST_DBG_TRAV, ST_DBG_LEAF, ST_DBG_INT, ST_DBG_SHADE,
+       // per traversal sub-step k < 16: lanes taking it (summed), waves executing it, lanes popping after it
+       ST_DBG_SUB, ST_TOTAL = ST_DBG_SUB + 48 };
+
+#ifdef SRT_PHASE_TIMING
+__device__ __forceinline__ void dbg_count(unsigned long long* stats, int idx, bool cond, bool waves) {
+  const unsigned long long m = __ballot(cond);
+  if (m && (threadIdx.x & 63) == 0) {
+    atomicAdd(&stats[idx], (unsigned long long)__popcll(m));
+    if (waves) atomicAdd(&stats[idx + 1], 1ull);
+  }
+}
+#define DBG_COUNT(stats, idx, cond) dbg_count(stats, idx, cond, ((idx) - ST_DBG_SUB) % 3 == 0)
+#else
+#define DBG_COUNT(stats, idx, cond)
+#endif
 
 // Diagnostic build only (-DSRT_PHASE_TIMING): per-wave shader-clock stamps at the
 // phase boundaries of sample_kernel, summed into stats[ST_CYC_*].
@@ -742,10 +757,13 @@ template <bool COUNT, bool LDSM, int K>
 __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln, Counters& c, Trav& t, bool any) {
   if constexpr (kStepPattern[K] != 0) {
     if constexpr (kStepPattern[K] == 'I') {
+      DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K, t.cnt == 0 && t.ref != kNoneRef);
       if (t.cnt == 0 && t.ref != kNoneRef) trav_internal<COUNT, LDSM>(kp, ln, c, t);
     } else {
+      DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K, t.cnt > 0);
       if (t.cnt > 0) trav_leaf<COUNT, LDSM>(kp, c, t, any);
     }
+    DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K + 2, t.active & !t.start & (t.cnt == 0) & (t.ref == kNoneRef));
     trav_pop<LDSM>(kp, ln, t, any);
     trav_substeps<COUNT, LDSM, K + 1>(kp, ln, c, t, any);
   }
@@ -1705,9 +1723,10 @@ int srt_finish(srt_context* c) {
 // out[0..3]: refill / traversal / shading cycles, outer iterations; out[4..9]: traversal
 // iterations and summed lane counts (working, traversing, at a leaf, at an internal node),
 // lanes shading (summed over outer iterations).
-extern "C" int srt_debug_phase_cycles(srt_context* c, unsigned long long out[10]) {
+// out[10..57]: per sub-step k (3 values): lanes taking it, waves executing it, lanes popping after it.
+extern "C" int srt_debug_phase_cycles(srt_context* c, unsigned long long out[58]) {
   if (!c || !out) return SRT_ERR_INVALID;
-  HIP_OK(hipMemcpyAsync(out, c->d_stats + srt::ST_CYC_REFILL, 10 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+  HIP_OK(hipMemcpyAsync(out, c->d_stats + srt::ST_CYC_REFILL, 58 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                         c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
   return SRT_OK;

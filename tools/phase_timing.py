@@ -11,7 +11,7 @@ r.render(spp); r.finish()
 r.render(spp); r.finish()
 lib = _lib.lib(); lib.srt_debug_phase_cycles.argtypes = [C.c_void_p, C.c_void_p]
 import numpy as np
-out = np.zeros(10, np.uint64)
+out = np.zeros(58, np.uint64)
 lib.srt_debug_phase_cycles(r.compute.ctx, out.ctypes.data)
 tot = out[:3].sum()
 print("kernel_ms", r.compute.last_kernel_ms(), "refill %.1f%% trav %.1f%% shade %.1f%% iters/wave %.0f" % (
@@ -19,3 +19,8 @@ print("kernel_ms", r.compute.last_kernel_ms(), "refill %.1f%% trav %.1f%% shade 
 ti, wk, tv, lf, it, sh = (float(v) for v in out[4:10])
 print("trav iters/wave %.0f  per iteration: working %.1f traversing %.1f leaf %.1f internal %.1f pop-only %.1f lanes;"
       " shading lanes/outer iter %.1f" % (ti / 4096, wk / ti, tv / ti, lf / ti, it / ti, (tv - lf - it) / ti, sh / float(out[3])))
+for k in range(16):
+    lanes, waves, pops = (float(v) for v in out[10 + 3 * k: 13 + 3 * k])
+    if waves:
+        print("  sub-step %2d: executed in %5.1f%% of iterations, %4.1f lanes when executed, %4.1f lanes pop after it"
+              % (k, 100 * waves / ti, lanes / waves, pops / ti))
