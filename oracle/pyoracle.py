@@ -65,6 +65,8 @@ def lib():
             getattr(L, fn).restype = C.c_float
         L.oracle_pow.argtypes = [C.c_float, C.c_float]
         L.oracle_pow.restype = C.c_float
+        L.oracle_pow5.argtypes = [C.c_float]
+        L.oracle_pow5.restype = C.c_float
         L.oracle_rand_float.argtypes = [C.c_float, C.c_float]
         L.oracle_rand_float.restype = C.c_float
         _lib = L
@@ -158,6 +160,10 @@ def cos(x):
 
 def pow(x, y):  # noqa: A001
     return lib().oracle_pow(float(x), float(y))
+
+
+def pow5(x):
+    return lib().oracle_pow5(float(x))
 
 
 def rand_float(sx, sy):

@@ -144,6 +144,19 @@ float oracle_pow(float x, float y) {
   return (float)exp2_d((double)y * log2_pos(x));
 }
 
+/* pow(x, 5.0) of the Fresnel terms (brdf.glsl:34-41): x^5 by multiplication in
+ * double (x^2 exact, x^4 and x^5 rounded), then rounded to float.  This is x^5
+ * rounded to nearest-even for every x whose result is a normal float (checked
+ * over all 2^32 inputs against the exact value: tools/pow5_exhaustive.hip).
+ * GLSL domain as oracle_pow: x < 0 and NaN -> NaN, +-0 -> +0. */
+float oracle_pow5(float x) {
+  if (!(x >= 0.0f)) return NAN;
+  if (x == 0.0f) return 0.0f;
+  const double d = (double)x;
+  const double d2 = d * d;
+  return (float)((d2 * d2) * d);
+}
+
 /* ------------------------------------------------------------------ */
 /* per-invocation context                                              */
 /* ------------------------------------------------------------------ */
@@ -230,12 +243,12 @@ static inline float shadowedF90(v3 F0) {
 }
 /* brdf.glsl:39-41 */
 static inline v3 fresnelSchlickNew(v3 f0, float f90, float NdotS) {
-  float p = oracle_pow(1.0f - NdotS, 5.0f);
+  float p = oracle_pow5(1.0f - NdotS);
   return add(f0, muls(V(f90 - f0.x, f90 - f0.y, f90 - f0.z), p));
 }
 /* brdf.glsl:34-36 */
 static inline v3 schlickFresnel(v3 f0, float u) {
-  float p = oracle_pow(fmx(0.001f, 1.0f - u), 5.0f);
+  float p = oracle_pow5(fmx(0.001f, 1.0f - u));
   return add(f0, muls(sub(V(1.0f, 1.0f, 1.0f), f0), p));
 }
 /* raytrace_utils.glsl:177-184 */

@@ -103,6 +103,7 @@ void oracle_trace_closest(const OrScene* s, uint32_t bvh_count, const OrRay* ray
 float oracle_sin(float x);
 float oracle_cos(float x);
 float oracle_pow(float x, float y);
+float oracle_pow5(float x);
 float oracle_rand_float(float sx, float sy);
 
 #ifdef __cplusplus

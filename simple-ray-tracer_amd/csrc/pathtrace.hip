@@ -191,11 +191,11 @@ __device__ __forceinline__ f3 perpendicular(f3 u) {
 }
 __device__ __forceinline__ float shadowedF90(f3 F0) { return fmn(1.0f, (1.0f / 0.04f) * luminance(F0)); }
 __device__ __forceinline__ f3 fresnelSchlickNew(f3 f0, float f90, float NdotS) {
-  const float p = pow_f(1.0f - NdotS, 5.0f);
+  const float p = pow5_f(1.0f - NdotS);
   return f0 + mk(f90 - f0.x, f90 - f0.y, f90 - f0.z) * p;
 }
 __device__ __forceinline__ f3 schlickFresnel(f3 f0, float u) {
-  const float p = pow_f(fmx(0.001f, 1.0f - u), 5.0f);
+  const float p = pow5_f(fmx(0.001f, 1.0f - u));
   return f0 + (mk(1.0f, 1.0f, 1.0f) - f0) * p;
 }
 __device__ __forceinline__ float linearToSrgb(float c) {

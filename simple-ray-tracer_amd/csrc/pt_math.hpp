@@ -9,7 +9,8 @@
 //     correctly rounded '/' and sqrt, denormals preserved;
 //   * GLSL min/max/clamp with IEEE minNum/maxNum NaN handling;
 //   * sin/cos: double Cody-Waite reduction + fdlibm-style polynomials, rounded
-//     to float; pow(x, y) = exp2(y * log2(x)) in double (x < 0 -> NaN).
+//     to float; pow(x, y) = exp2(y * log2(x)) in double (x < 0 -> NaN);
+//   * pow(x, 5.0) = x^5 rounded to nearest-even (pow5_f).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -133,6 +134,19 @@ __device__ __forceinline__ float pow_f(float x, float y) {
   if (x == 0.0f) return (y > 0.0f) ? 0.0f : (y == 0.0f ? __builtin_nanf("") : __builtin_inff());
   if (x == __builtin_inff()) return (y > 0.0f) ? __builtin_inff() : (y == 0.0f ? __builtin_nanf("") : 0.0f);
   return (float)exp2_d((double)y * log2_pos(x));
+}
+
+// pow(x, 5.0) (the Fresnel terms, brdf.glsl): x^5 by multiplication in
+// double -- x^2 exact, x^4 and x^5 rounded to double -- then rounded to float.
+// GLSL domain as pow_f: x < 0 and NaN give NaN, +-0 gives +0.  It differs from
+// pow_f(x, 5.0f) = exp2(5 * log2(x)) in 92 of 2^32 inputs, all exact float
+// midpoints such as x = 1.8125, where this form rounds half to even
+// (tools/pow5_exhaustive.hip).
+__device__ __forceinline__ float pow5_f(float x) {
+  if (!(x >= 0.0f)) return __builtin_nanf("");
+  const double d = (double)x;
+  const double d2 = d * d;
+  return x == 0.0f ? 0.0f : (float)((d2 * d2) * d);
 }
 
 }  // namespace dev

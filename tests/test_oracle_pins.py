@@ -37,6 +37,33 @@ def test_pow_accuracy_and_glsl_domain():
     assert math.isnan(O.pow(float("nan"), 5.0))
 
 
+def _rn32_pow5(x):
+    """x^5 rounded to nearest-even fp32, from the exact integer value (normal results only)."""
+    m, e = math.frexp(float(x))          # x = m * 2^e, 0.5 <= m < 1
+    mi = int(m * (1 << 24))              # 24-bit integer mantissa: x = mi * 2^(e - 24)
+    p = mi ** 5
+    shift = p.bit_length() - 24
+    q, rem = p >> shift, p & ((1 << shift) - 1)
+    half = 1 << (shift - 1)
+    if rem > half or (rem == half and q & 1):
+        q += 1
+    return float(np.float32(math.ldexp(q, shift + 5 * (e - 24))))
+
+
+def test_pow5_is_correctly_rounded():
+    """pow(x, 5.0) of the Fresnel terms: x^5 rounded to nearest-even."""
+    rng = np.random.default_rng(5)
+    xs = np.concatenate([rng.uniform(0.001, 1.0, 4000), rng.uniform(1.0, 30.0, 1000),
+                         np.array([1.8125, 0.90625, 0.453125, 29.0, 0.001, 1.0, 0.5])]).astype(np.float32)
+    for x in xs:
+        assert O.pow5(float(x)) == _rn32_pow5(x), x
+    # 1.8125^5 = 29^5 / 2^20 lies exactly halfway between two floats: ties to even
+    assert O.pow5(1.8125) == _rn32_pow5(1.8125) == float(np.float32(20511148 / 2**20))
+    assert math.isnan(O.pow5(-0.25)) and math.isnan(O.pow5(float("nan")))
+    assert O.pow5(0.0) == 0.0 and math.copysign(1.0, O.pow5(-0.0)) == 1.0
+    assert O.pow5(float("inf")) == float("inf") and O.pow5(1e30) == float("inf")
+
+
 def test_rand_float_is_fract_of_scaled_sin():
     for sx, sy in ((0.0, 0.0), (1.25, -3.5), (17.0, 9.0), (-8.7238, 5.9055)):
         d = np.float32(np.float32(sx) * np.float32(12.9898)) + np.float32(np.float32(sy) * np.float32(78.233))
