@@ -53,30 +53,27 @@ static inline int f2i(float x) {
 }
 static inline v3 vload(const float* p) { return V(p[0], p[1], p[2]); }
 
-/* ---- sin / cos: double-precision Cody-Waite reduction + polynomials ---- */
-static const double kTwoOverPi = 0x1.45f306dc9c883p-1;
-static const double kPio2_1 = 0x1.921fb54400000p+0;
-static const double kPio2_1t = 0x1.0b4611a626331p-34;
-static const double kS1 = -1.66666666666666324348e-01, kS2 = 8.33333333332248946124e-03,
-                    kS3 = -1.98412698298579493134e-04, kS4 = 2.75573137070700676789e-06,
-                    kS5 = -2.50507602534068634195e-08, kS6 = 1.58969099521155010221e-10;
-static const double kC1 = 4.16666666666666019037e-02, kC2 = -1.38888888888741095749e-03,
-                    kC3 = 2.48015872894767294178e-05, kC4 = -2.75573143513906633035e-07,
-                    kC5 = 2.08757232129817482790e-09, kC6 = -1.13596475577881948265e-11;
-
-static void sincos_kernel(float xf, int want_cos, float* out) {
-  if (xf != xf || xf == INFINITY || xf == -INFINITY) { *out = NAN; return; }
-  if (fabsf(xf) >= 1073741824.0f) { *out = 0.0f; return; }
-  double x = (double)xf;
-  double kd = rint(x * kTwoOverPi);
-  long long k = (long long)kd;
-  double r = (x - kd * kPio2_1) - kd * kPio2_1t;
-  double z = r * r;
-  double s = r + (r * z) * (kS1 + z * (kS2 + z * (kS3 + z * (kS4 + z * (kS5 + z * kS6)))));
-  double c = (1.0 - 0.5 * z) + (z * z) * (kC1 + z * (kC2 + z * (kC3 + z * (kC4 + z * (kC5 + z * kC6)))));
-  int q = (int)((k + (want_cos ? 1 : 0)) & 3);
-  double v = (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
-  *out = (float)v;
+/* ---- sin / cos -----------------------------------
+ * fp32 with fused multiply-adds: k = rint(x * 2/pi); r = x - k * pi/2 with
+ * pi/2 = P1 + P2 + P3 (each product exact inside its fmaf); then the Cephes
+ * sinf/cosf minimax polynomials on [-pi/4, pi/4] and the quadrant's
+ * sign/selection.  |x| >= 2^30 gives 0, NaN and Inf give NaN.  The kernel
+ * (simple-ray-tracer_amd/csrc/pt_math.hpp) evaluates the same expressions. */
+static void sincos_kernel(float x, int want_cos, float* out) {
+  if (x != x || x == INFINITY || x == -INFINITY) { *out = NAN; return; }
+  if (fabsf(x) >= 0x1p30f) { *out = 0.0f; return; }
+  const float kf = rintf(x * 0x1.45f306p-1f);
+  float r = fmaf(-kf, 0x1.921fb6p+0f, x);
+  r = fmaf(-kf, -0x1.777a5cp-25f, r);
+  r = fmaf(-kf, -0x1.ee59dap-50f, r);
+  const float z = r * r;
+  const float ps = fmaf(fmaf(-0x1.9943f2p-13f, z, 0x1.11073cp-7f), z, -0x1.555546p-3f);
+  const float s = fmaf(ps * z, r, r);
+  const float pc = fmaf(fmaf(0x1.99eb9cp-16f, z, -0x1.6c0c34p-10f), z, 0x1.55554ap-5f);
+  const float c = fmaf(pc * z, z, fmaf(-0.5f, z, 1.0f));
+  const int q = ((int)kf + (want_cos ? 1 : 0)) & 3;
+  const float v = (q & 1) ? c : s;
+  *out = (q & 2) ? -v : v;
 }
 float oracle_sin(float x) { float r; sincos_kernel(x, 0, &r); return r; }
 float oracle_cos(float x) { float r; sincos_kernel(x, 1, &r); return r; }

@@ -8,8 +8,8 @@
 //   * IEEE fp32, source-order evaluation, no FMA contraction (-ffp-contract=off),
 //     correctly rounded '/' and sqrt, denormals preserved;
 //   * GLSL min/max/clamp with IEEE minNum/maxNum NaN handling;
-//   * sin/cos: double Cody-Waite reduction + fdlibm-style polynomials, rounded
-//     to float; pow(x, y) = exp2(y * log2(x)) in double (x < 0 -> NaN);
+//   * sin/cos: fp32 Cody-Waite reduction with FMA + minimax polynomials (below);
+//     pow(x, y) = exp2(y * log2(x)) in double (x < 0 -> NaN);
 //   * pow(x, 5.0) = x^5 rounded to nearest-even (pow5_f).
 #pragma once
 
@@ -54,26 +54,27 @@ __device__ __forceinline__ int f2i(float x) {
 __device__ __forceinline__ bool isinf_f(float x) { return __builtin_fabsf(x) == __builtin_inff(); }
 
 // ---- sin / cos ------------------------------------------------------------
-__device__ __forceinline__ float sincos_kernel(float xf, int want_cos) {
-  if (xf != xf || isinf_f(xf)) return __builtin_nanf("");
-  if (__builtin_fabsf(xf) >= 1073741824.0f) return 0.0f;
-  const double kTwoOverPi = 0x1.45f306dc9c883p-1;
-  const double kPio2_1 = 0x1.921fb54400000p+0;
-  const double kPio2_1t = 0x1.0b4611a626331p-34;
-  const double x = (double)xf;
-  const double kd = __builtin_rint(x * kTwoOverPi);
-  const long long k = (long long)kd;
-  const double r = (x - kd * kPio2_1) - kd * kPio2_1t;
-  const double z = r * r;
-  const double s = r + (r * z) * (-1.66666666666666324348e-01 + z * (8.33333333332248946124e-03 +
-                   z * (-1.98412698298579493134e-04 + z * (2.75573137070700676789e-06 +
-                   z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)))));
-  const double c = (1.0 - 0.5 * z) + (z * z) * (4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 +
-                   z * (2.48015872894767294178e-05 + z * (-2.75573143513906633035e-07 +
-                   z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
-  const int q = (int)((k + want_cos) & 3);
-  const double v = (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
-  return (float)v;
+// The contract's sin/cos, in fp32 with fused multiply-adds:
+// k = rint(x * 2/pi); r = x - k * pi/2 with pi/2 = P1 + P2 + P3 (each product
+// exact inside its FMA); then minimax polynomials on [-pi/4, pi/4] (Cephes
+// sinf/cosf coefficients) and the quadrant's sign/selection.  |x| >= 2^30
+// gives 0, NaN and Inf give NaN.  oracle/srt_oracle.c evaluates the same
+// expressions with fmaf/rintf.
+__device__ __forceinline__ float sincos_kernel(float x, int want_cos) {
+  if (x != x || isinf_f(x)) return __builtin_nanf("");
+  if (__builtin_fabsf(x) >= 0x1p30f) return 0.0f;
+  const float kf = __builtin_rintf(x * 0x1.45f306p-1f);
+  float r = __builtin_fmaf(-kf, 0x1.921fb6p+0f, x);
+  r = __builtin_fmaf(-kf, -0x1.777a5cp-25f, r);
+  r = __builtin_fmaf(-kf, -0x1.ee59dap-50f, r);
+  const float z = r * r;
+  const float ps = __builtin_fmaf(__builtin_fmaf(-0x1.9943f2p-13f, z, 0x1.11073cp-7f), z, -0x1.555546p-3f);
+  const float s = __builtin_fmaf(ps * z, r, r);
+  const float pc = __builtin_fmaf(__builtin_fmaf(0x1.99eb9cp-16f, z, -0x1.6c0c34p-10f), z, 0x1.55554ap-5f);
+  const float c = __builtin_fmaf(pc * z, z, __builtin_fmaf(-0.5f, z, 1.0f));
+  const int q = ((int)kf + want_cos) & 3;
+  const float v = (q & 1) ? c : s;
+  return (q & 2) ? -v : v;
 }
 __device__ __forceinline__ float sin_f(float x) { return sincos_kernel(x, 0); }
 __device__ __forceinline__ float cos_f(float x) { return sincos_kernel(x, 1); }
