@@ -66,6 +66,8 @@ struct KParams {
   int local_pixels;        // W * local_rows
   int trav_frac16;         // resume shading when fewer than trav_frac16/16 of working lanes traverse
   int stack_base_f4;       // first float4 of the per-lane stacks in dynamic LDS
+  uint32_t* gstack;        // global-scene mode: per-lane stacks in HBM, entry field k of lane g at gstack[k * stride + g]
+  int gstack_stride;       // lanes in the grid
   float cx, cy, cz, p00x, p00y, p00z, dux, duy, duz, dvx, dvy, dvz;
 };
 
@@ -79,7 +81,8 @@ enum { ST_RAYS = 0, ST_NODES, ST_TRIS, ST_RNGU, ST_RNGSQ, ST_LIGHTS, ST_MATS, ST
        // per traversal sub-step k < 16: lanes taking it (summed), waves executing it, lanes popping after it
        ST_DBG_SUB, ST_TOTAL = ST_DBG_SUB + 48 };
 
-#ifdef SRT_PHASE_TIMING
+// Diagnostic build only (-DSRT_SUBSTEP_STATS): per-sub-step lane counts (global atomics, slow).
+#ifdef SRT_SUBSTEP_STATS
 __device__ __forceinline__ void dbg_count(unsigned long long* stats, int idx, bool cond, bool waves) {
   const unsigned long long m = __ballot(cond);
   if (m && (threadIdx.x & 63) == 0) {
@@ -786,7 +789,13 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
 }
 
 template <bool COUNT, bool LDSM, int BLOCK>
-__global__ __launch_bounds__(BLOCK) void sample_kernel(KParams kp) {
+#ifndef SRT_GLOBAL_WAVES
+#define SRT_GLOBAL_WAVES 4
+#endif
+// waves per SIMD the register allocation must allow: 4 (<= 128 VGPRs) in LDS
+// mode, where the 1024-thread block's LDS caps residency at 4 anyway;
+// SRT_GLOBAL_WAVES in global-scene mode, whose HBM latency wants more waves
+__global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_kernel(KParams kp) {
   const int tid = threadIdx.x;
   if constexpr (LDSM) {  // the block copies the scene (nodes + triangles) into LDS once
     const int total = kp.nodes_f4 + kp.tris_f4;
@@ -798,8 +807,13 @@ __global__ __launch_bounds__(BLOCK) void sample_kernel(KParams kp) {
   const int n_waves = (int)(gridDim.x * (blockDim.x >> 6));
   const int wave_id = (int)(blockIdx.x * (blockDim.x >> 6)) + (tid >> 6);
   Lane ln;
-  ln.stk = reinterpret_cast<uint32_t*>(g_smem + kp.stack_base_f4) + tid;
-  ln.stride = blockDim.x;
+  if constexpr (LDSM) {
+    ln.stk = reinterpret_cast<uint32_t*>(g_smem + kp.stack_base_f4) + tid;
+    ln.stride = blockDim.x;
+  } else {  // lane-interleaved: a wave's pushes and pops are coalesced 256-B accesses
+    ln.stk = kp.gstack + (size_t)blockIdx.x * BLOCK + tid;
+    ln.stride = kp.gstack_stride;
+  }
   ln.base = 0;
   Counters c;
   for (int k = 0; k < ST_N; ++k) c.v[k] = 0;
@@ -1281,6 +1295,8 @@ struct srt_context {
   int img_w = 0, img_rows = 0;
   // sample buffer (nframes x local pixels float4)
   float4* d_lbuf = nullptr;
+  uint32_t* d_gstack = nullptr;  // global-scene mode traversal stacks
+  size_t gstack_bytes = 0;
   size_t lbuf_bytes = 0;
   size_t lbuf_cap = (size_t)16 << 30;  // SRT_SAMPLE_BUFFER_MB
   int trav_frac16 = 8;                 // SRT_TRAV_FRAC16 (measured best on Rubik 1080p with 2-triangle leaf steps)
@@ -1428,11 +1444,24 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
 constexpr size_t kLdsBytes = 160 * 1024;
 
 template <bool COUNT, bool LDSM, int BLOCK>
-int LaunchSamples(srt_context* c, const srt::KParams& kp, size_t lds) {
+int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
   int per_cu = 0;
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sample_kernel<COUNT, LDSM, BLOCK>, BLOCK, lds));
   per_cu = std::max(per_cu, 1);
   const int blocks = c->num_cus * per_cu;
+  if constexpr (!LDSM) {  // global-scene mode: 3-dword stack entries per lane in HBM
+    const size_t lanes = (size_t)blocks * BLOCK;
+    const size_t need = lanes * 3 * sizeof(uint32_t) * (size_t)kp.stack_entries;
+    if (need > c->gstack_bytes) {
+      FreeDev(c->d_gstack);
+      c->d_gstack = nullptr;
+      c->gstack_bytes = 0;
+      HIP_OK(hipMalloc(&c->d_gstack, need));
+      c->gstack_bytes = need;
+    }
+    kp.gstack = c->d_gstack;
+    kp.gstack_stride = (int)lanes;
+  }
   hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM, BLOCK>), dim3(blocks), dim3(BLOCK), lds, c->stream, kp);
   HIP_OK(hipGetLastError());
   return SRT_OK;
@@ -1460,9 +1489,9 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   if (ldsm) {
     kp.stack_base_f4 = kp.nodes_f4 + kp.tris_f4;
     lds = lds_mode_bytes;
-  } else {
+  } else {  // stacks in HBM (LaunchSamples): no LDS, occupancy set by registers
     kp.stack_base_f4 = 0;
-    lds = (size_t)block * 3 * sizeof(uint32_t) * (size_t)kp.stack_entries;
+    lds = 0;
   }
   // sample buffer: as many frames per chunk as the buffer cap allows
   const size_t per_frame = (size_t)npx * sizeof(float4);
@@ -1609,7 +1638,7 @@ int srt_destroy(srt_context* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   FreeDev(c->d_nodes); FreeDev(c->d_tris); FreeDev(c->d_mats); FreeDev(c->d_bvhs); FreeDev(c->d_lights);
-  FreeDev(c->d_noise_xy); FreeDev(c->d_noise_u); FreeDev(c->d_stats); FreeDev(c->d_lbuf);
+  FreeDev(c->d_noise_xy); FreeDev(c->d_noise_u); FreeDev(c->d_stats); FreeDev(c->d_lbuf); FreeDev(c->d_gstack);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (!c->images_external) { FreeDev(c->d_accum); FreeDev(c->d_out); }
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
