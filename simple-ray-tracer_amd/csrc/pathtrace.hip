@@ -151,8 +151,10 @@ __device__ __forceinline__ void sphere_data(int i, f3& pos, float& radius, Mat& 
 // ---------------------------------------------------------------------------
 struct Lane {
   int base;             // (y * Height) + x  (raytrace_utils.glsl:11-12,45-46)
-  uint32_t* stk;        // LDS stack: entry k field f at stk[(3k+f) * stride]
+  uint32_t* stk;        // LDS stack: entry k field f at stk[(Fk+f) * stride] (global-scene mode: a ring of kShortStack)
   int stride;
+  uint32_t* gstk;       // global-scene mode: the whole stack in HBM, same layout
+  int gstride;
 };
 
 // (a % m) for 0 <= a, 0 < m, with the common case a < 2m handled by one compare
@@ -277,6 +279,33 @@ __device__ __forceinline__ void stk_ref(const Lane& ln, int sp, uint32_t& ref, u
   } else {
     ref = ln.stk[(3 * sp + 0) * ln.stride];
     cnt = ln.stk[(3 * sp + 1) * ln.stride];
+  }
+}
+// Entry `slot` of a lane-interleaved stack area (LDS or HBM): field k of the
+// entry at base[(F * slot + k) * stride], F = 2 (PACK: ref | count << 24, t) or 3.
+template <bool PACK>
+__device__ __forceinline__ void slot_write(uint32_t* base, int stride, int slot, uint32_t ref, uint32_t cnt, float t) {
+  if constexpr (PACK) {
+    base[(2 * slot + 0) * stride] = ref | (cnt << 24);
+    base[(2 * slot + 1) * stride] = __float_as_uint(t);
+  } else {
+    base[(3 * slot + 0) * stride] = ref;
+    base[(3 * slot + 1) * stride] = cnt;
+    base[(3 * slot + 2) * stride] = __float_as_uint(t);
+  }
+}
+template <bool PACK>
+__device__ __forceinline__ void slot_read(const uint32_t* base, int stride, int slot, uint32_t& ref, uint32_t& cnt,
+                                          float& t) {
+  if constexpr (PACK) {
+    const uint32_t w = base[(2 * slot + 0) * stride];
+    ref = w & 0xFFFFFFu;
+    cnt = w >> 24;
+    t = __uint_as_float(base[(2 * slot + 1) * stride]);
+  } else {
+    ref = base[(3 * slot + 0) * stride];
+    cnt = base[(3 * slot + 1) * stride];
+    t = __uint_as_float(base[(3 * slot + 2) * stride]);
   }
 }
 
@@ -646,6 +675,7 @@ struct Trav {
   uint32_t hit;       // best triangle so far (0xFFFFFFFF: none)
   uint32_t bi;        // current BVH
   int sp;
+  int lo;             // global-scene mode: entries [lo, sp) are in the LDS ring, [0, lo) in HBM
   bool active;        // still traversing
   bool start;         // next step sets up BVH `bi`
 };
@@ -661,6 +691,12 @@ constexpr int kLeafTris = SRT_LEAF_TRIS;  // triangles tested per leaf step
 #define SRT_STEP_PATTERN "ILILILIL"
 #endif
 constexpr char kStepPattern[] = SRT_STEP_PATTERN;
+// global-scene mode: entries per lane kept in the LDS ring (power of two)
+#ifndef SRT_SHORT_STACK
+#define SRT_SHORT_STACK 16
+#endif
+constexpr int kShortStack = SRT_SHORT_STACK;
+static_assert((kShortStack & (kShortStack - 1)) == 0, "kShortStack must be a power of two");
 constexpr int kTriPad = 3;                // zero records past the triangle array (>= kLeafTris - 1)
 static_assert(kLeafTris >= 1 && kLeafTris - 1 <= kTriPad, "kLeafTris");
 
@@ -679,6 +715,7 @@ __device__ __forceinline__ void trav_begin_bvh(const KParams& kp, Counters& c, T
   t.ref = ok ? __float_as_uint(rlo.w) : kNoneRef;
   t.cnt = ok ? __float_as_uint(rhi.w) : 0u;
   t.sp = 0;
+  t.lo = 0;
   t.start = false;
 }
 
@@ -713,7 +750,7 @@ __device__ __forceinline__ void trav_leaf(const KParams& kp, Counters& c, Trav& 
 
 // Internal sub-step: test both children's boxes; push c0 when both pass, go to
 // c1 if it passes, else to c0 if it passes.
-template <bool COUNT, bool LDSM>
+template <bool COUNT, bool LDSM, bool PACK>
 __device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln, Counters& c, Trav& t) {
   const uint32_t pi = 2 * t.ref + 2;
   const float4 l0 = node4<LDSM>(kp, pi), h0 = node4<LDSM>(kp, pi + 1);
@@ -725,7 +762,18 @@ __device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln,
   const uint32_t r0 = __float_as_uint(l0.w), n0 = __float_as_uint(h0.w);
   // the c0 slot is written unconditionally (it is free either way; the stack
   // holds depth + 1 entries, validated at upload)
-  stk_push<LDSM>(ln, t.sp, r0, n0, b0);
+  if constexpr (LDSM) {
+    slot_write<true>(ln.stk, ln.stride, t.sp, r0, n0, b0);
+  } else {
+    if (t.sp - t.lo == kShortStack) {  // ring full: its oldest entry moves to HBM (rare)
+      uint32_t r, n;
+      float bt;
+      slot_read<PACK>(ln.stk, ln.stride, t.lo & (kShortStack - 1), r, n, bt);
+      slot_write<PACK>(ln.gstk, ln.gstride, t.lo, r, n, bt);
+      ++t.lo;
+    }
+    slot_write<PACK>(ln.stk, ln.stride, t.sp & (kShortStack - 1), r0, n0, b0);
+  }
   t.sp += (v0 & v1) ? 1 : 0;
   if constexpr (COUNT) {
     if ((uint32_t)t.sp > c.v[ST_MAXSTACK]) c.v[ST_MAXSTACK] = (uint32_t)t.sp;
@@ -737,14 +785,22 @@ __device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln,
 // Nothing current: pop one entry (visited if it still beats the running
 // distance), or finish this BVH.  A lane whose next BVH is pending (`start`,
 // set up at the next iteration) does nothing.
-template <bool LDSM>
+template <bool LDSM, bool PACK>
 __device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav& t, bool any) {
   if (t.active & !t.start & (t.cnt == 0) & (t.ref == kNoneRef)) {
     if (t.sp > 0) {
       --t.sp;
-      const bool take = stk_t<LDSM>(ln, t.sp) < t.dist;
       uint32_t r, n;
-      stk_ref<LDSM>(ln, t.sp, r, n);
+      float et;
+      if constexpr (LDSM) {
+        slot_read<true>(ln.stk, ln.stride, t.sp, r, n, et);
+      } else if (t.sp < t.lo) {  // below the LDS ring: from HBM (rare)
+        slot_read<PACK>(ln.gstk, ln.gstride, t.sp, r, n, et);
+        t.lo = t.sp;
+      } else {
+        slot_read<PACK>(ln.stk, ln.stride, t.sp & (kShortStack - 1), r, n, et);
+      }
+      const bool take = et < t.dist;
       t.ref = take ? r : kNoneRef;
       t.cnt = take ? n : 0u;
     } else if ((any && t.hit != kNoneRef) || t.bi + 1 >= kp.bvh_count) {
@@ -756,19 +812,19 @@ __device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav
   }
 }
 
-template <bool COUNT, bool LDSM, int K>
+template <bool COUNT, bool LDSM, bool PACK, int K>
 __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln, Counters& c, Trav& t, bool any) {
   if constexpr (kStepPattern[K] != 0) {
     if constexpr (kStepPattern[K] == 'I') {
       DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K, t.cnt == 0 && t.ref != kNoneRef);
-      if (t.cnt == 0 && t.ref != kNoneRef) trav_internal<COUNT, LDSM>(kp, ln, c, t);
+      if (t.cnt == 0 && t.ref != kNoneRef) trav_internal<COUNT, LDSM, PACK>(kp, ln, c, t);
     } else {
       DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K, t.cnt > 0);
       if (t.cnt > 0) trav_leaf<COUNT, LDSM>(kp, c, t, any);
     }
     DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K + 2, t.active & !t.start & (t.cnt == 0) & (t.ref == kNoneRef));
-    trav_pop<LDSM>(kp, ln, t, any);
-    trav_substeps<COUNT, LDSM, K + 1>(kp, ln, c, t, any);
+    trav_pop<LDSM, PACK>(kp, ln, t, any);
+    trav_substeps<COUNT, LDSM, PACK, K + 1>(kp, ln, c, t, any);
   }
 }
 
@@ -777,18 +833,18 @@ __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln,
 // node is of its kind, so a lane makes up to strlen(kStepPattern) steps of
 // its own sequence per iteration, in order.  `any` selects the shadow-ray
 // (first hit) variant.
-template <bool COUNT, bool LDSM>
+template <bool COUNT, bool LDSM, bool PACK>
 __device__ __forceinline__ void trav_step(const KParams& kp, const Lane& ln, Counters& c, Trav& t, f3 ro, f3 rd,
                                           bool any) {
   if (t.start) trav_begin_bvh<COUNT, LDSM>(kp, c, t, ro, rd);  // only for BVHs after the first
-  trav_substeps<COUNT, LDSM, 0>(kp, ln, c, t, any);
+  trav_substeps<COUNT, LDSM, PACK, 0>(kp, ln, c, t, any);
 }
 
 __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
   return __popcll(mask & ((1ull << lane) - 1ull));
 }
 
-template <bool COUNT, bool LDSM, int BLOCK>
+template <bool COUNT, bool LDSM, bool PACK, int BLOCK>
 #ifndef SRT_GLOBAL_WAVES
 #define SRT_GLOBAL_WAVES 4
 #endif
@@ -810,9 +866,11 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
   if constexpr (LDSM) {
     ln.stk = reinterpret_cast<uint32_t*>(g_smem + kp.stack_base_f4) + tid;
     ln.stride = blockDim.x;
-  } else {  // lane-interleaved: a wave's pushes and pops are coalesced 256-B accesses
-    ln.stk = kp.gstack + (size_t)blockIdx.x * BLOCK + tid;
-    ln.stride = kp.gstack_stride;
+  } else {  // the top kShortStack entries in an LDS ring, the rest in HBM (lane-interleaved, coalesced)
+    ln.stk = reinterpret_cast<uint32_t*>(g_smem) + tid;
+    ln.stride = BLOCK;
+    ln.gstk = kp.gstack + (size_t)blockIdx.x * BLOCK + tid;
+    ln.gstride = kp.gstack_stride;
   }
   ln.base = 0;
   Counters c;
@@ -940,7 +998,7 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
         d_leaf += __popcll(__ballot(tr.active && tr.cnt > 0));
         d_int += __popcll(__ballot(tr.active && tr.cnt == 0 && tr.ref != kNoneRef));
 #endif
-        if (tr.active) trav_step<COUNT, LDSM>(kp, ln, c, tr, ro, rd, shadow_phase);
+        if (tr.active) trav_step<COUNT, LDSM, PACK>(kp, ln, c, tr, ro, rd, shadow_phase);
       }
     }
 
@@ -1443,15 +1501,16 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
 // LDS budget per CU (gfx950: 160 KiB; one 1024-thread block per CU in LDS mode)
 constexpr size_t kLdsBytes = 160 * 1024;
 
-template <bool COUNT, bool LDSM, int BLOCK>
+template <bool COUNT, bool LDSM, bool PACK, int BLOCK>
 int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
   int per_cu = 0;
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sample_kernel<COUNT, LDSM, BLOCK>, BLOCK, lds));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sample_kernel<COUNT, LDSM, PACK, BLOCK>, BLOCK,
+                                                        lds));
   per_cu = std::max(per_cu, 1);
   const int blocks = c->num_cus * per_cu;
-  if constexpr (!LDSM) {  // global-scene mode: 3-dword stack entries per lane in HBM
+  if constexpr (!LDSM) {  // global-scene mode: every lane's full stack in HBM (backing the LDS ring)
     const size_t lanes = (size_t)blocks * BLOCK;
-    const size_t need = lanes * 3 * sizeof(uint32_t) * (size_t)kp.stack_entries;
+    const size_t need = lanes * (PACK ? 2 : 3) * sizeof(uint32_t) * (size_t)kp.stack_entries;
     if (need > c->gstack_bytes) {
       FreeDev(c->d_gstack);
       c->d_gstack = nullptr;
@@ -1462,7 +1521,7 @@ int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
     kp.gstack = c->d_gstack;
     kp.gstack_stride = (int)lanes;
   }
-  hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM, BLOCK>), dim3(blocks), dim3(BLOCK), lds, c->stream, kp);
+  hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM, PACK, BLOCK>), dim3(blocks), dim3(BLOCK), lds, c->stream, kp);
   HIP_OK(hipGetLastError());
   return SRT_OK;
 }
@@ -1489,9 +1548,9 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   if (ldsm) {
     kp.stack_base_f4 = kp.nodes_f4 + kp.tris_f4;
     lds = lds_mode_bytes;
-  } else {  // stacks in HBM (LaunchSamples): no LDS, occupancy set by registers
+  } else {  // LDS rings of kShortStack entries per lane, backed by HBM stacks (LaunchSamples)
     kp.stack_base_f4 = 0;
-    lds = 0;
+    lds = (size_t)block * (c->lds_ok ? 2 : 3) * sizeof(uint32_t) * (size_t)srt::kShortStack;
   }
   // sample buffer: as many frames per chunk as the buffer cap allows
   const size_t per_frame = (size_t)npx * sizeof(float4);
@@ -1522,10 +1581,15 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
     kc.write_output = (f0 + chunk >= kp.nframes) ? kp.write_output : 0;
     int rc;
     HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
-    if (count && ldsm) rc = block == 512 ? LaunchSamples<true, true, 512>(c, kc, lds) : LaunchSamples<true, true, 1024>(c, kc, lds);
-    else if (count) rc = LaunchSamples<true, false, 256>(c, kc, lds);
-    else if (ldsm) rc = block == 512 ? LaunchSamples<false, true, 512>(c, kc, lds) : LaunchSamples<false, true, 1024>(c, kc, lds);
-    else rc = LaunchSamples<false, false, 256>(c, kc, lds);
+    // LDS mode: packed entries (lds_ok); global-scene mode: packed when indices fit 24 bits
+    const bool pack = c->lds_ok;
+    if (count && ldsm) rc = block == 512 ? LaunchSamples<true, true, true, 512>(c, kc, lds)
+                                         : LaunchSamples<true, true, true, 1024>(c, kc, lds);
+    else if (count) rc = pack ? LaunchSamples<true, false, true, 256>(c, kc, lds)
+                              : LaunchSamples<true, false, false, 256>(c, kc, lds);
+    else if (ldsm) rc = block == 512 ? LaunchSamples<false, true, true, 512>(c, kc, lds)
+                                     : LaunchSamples<false, true, true, 1024>(c, kc, lds);
+    else rc = pack ? LaunchSamples<false, false, true, 256>(c, kc, lds) : LaunchSamples<false, false, false, 256>(c, kc, lds);
     if (rc) return rc;
     HIP_OK(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
     c->ev_used += 2;
