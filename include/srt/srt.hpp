@@ -135,6 +135,10 @@ class Compute {
     check(srt_read_output(context(), v.data(), v.size()), "ReadOutput");
     return v;
   }
+  // output stage: image0 to a PNG / PPM file, top row first (as the window shows it)
+  void SaveImage(const std::string& path, bool flip_y = true) {
+    check(srt_write_output(context(), path.c_str(), flip_y ? 1 : 0), "SaveImage");
+  }
   void SetWidthHint(int w) { width_ = w; }
   int width() const { return width_; }
 

@@ -134,6 +134,13 @@ int srt_alloc_images(srt_context* ctx);
 int srt_read_accum(srt_context* ctx, float* host_rgba32f, size_t bytes);
 int srt_read_output(srt_context* ctx, uint8_t* host_rgba8, size_t bytes);
 int srt_write_accum(srt_context* ctx, const float* host_rgba32f, size_t bytes);
+/* Output stage (replaces the GL display quad, src/main.cpp:303-349): write an
+ * RGBA8 image to `path`, PNG (RGBA) or binary PPM (RGB) by extension.
+ * flip_y != 0 writes the kernel's bottom row (j = 0) last, as displayed.
+ * SRT_ERR_IO on a file error, SRT_ERR_INVALID for an unknown extension. */
+int srt_image_write(const char* path, const uint8_t* rgba8, int width, int height, int flip_y);
+/* The context's current image0 (its local rows) through srt_image_write. */
+int srt_write_output(srt_context* ctx, const char* path, int flip_y);
 /* Device pointers of the images (for RCCL gathers without a host copy). */
 int srt_image_pointers(srt_context* ctx, void** accum_dev, void** out_dev);
 /* Use caller-owned device buffers (>= local_rows * Width RGBA32F / RGBA8) as

@@ -2018,6 +2018,14 @@ int srt_read_output(srt_context* c, uint8_t* host, size_t bytes) {
   return SRT_OK;
 }
 
+int srt_write_output(srt_context* c, const char* path, int flip_y) {
+  if (!c || !path || !c->d_out || c->img_w <= 0 || c->img_rows <= 0) return SRT_ERR_INVALID;
+  std::vector<uint8_t> px((size_t)c->img_w * c->img_rows * 4);
+  const int rc = srt_read_output(c, px.data(), px.size());
+  if (rc) return rc;
+  return srt_image_write(path, px.data(), c->img_w, c->img_rows, flip_y);
+}
+
 int srt_set_image_buffers(srt_context* c, void* accum_dev, void* out_dev) {
   if (!c || !accum_dev || !out_dev || c->W <= 0 || c->H <= 0) return SRT_ERR_INVALID;
   if (!c->images_external) { FreeDev(c->d_accum); FreeDev(c->d_out); }

@@ -131,6 +131,15 @@ def glibc_rand(n: int) -> np.ndarray:
     return out
 
 
+def write_image(path: str | pathlib.Path, rgba8: np.ndarray, flip_y: bool = True) -> None:
+    """Output stage (replaces the GL display quad, src/main.cpp:303-349): an (H, W, 4) uint8 image
+    to PNG (RGBA) or binary PPM (RGB) by extension.  flip_y writes the kernel's bottom row last."""
+    a = np.ascontiguousarray(rgba8, np.uint8)
+    if a.ndim != 3 or a.shape[2] != 4:
+        raise ValueError("write_image expects an (H, W, 4) uint8 array")
+    check(lib().srt_image_write(str(path).encode(), _ptr(a), a.shape[1], a.shape[0], int(flip_y)), "srt_image_write")
+
+
 def generate_noise(width: int, height: int, gcc_order: bool = True) -> tuple[np.ndarray, np.ndarray]:
     """UpdateNoiseTex (src/main.cpp:269-301): W*H unit vectors, then W*H uniform vec3s (RGB32F)."""
     texels = int(width) * int(height)
@@ -395,6 +404,10 @@ class Compute:
         a = np.zeros((rows, self.width, 4), np.uint8)
         check(lib().srt_read_output(self.ctx, _ptr(a), a.nbytes), "read_output")
         return a
+
+    def save_image(self, path: str | pathlib.Path, flip_y: bool = True) -> None:
+        """image0 (the local rows) to a PNG / PPM file (write_image)."""
+        check(lib().srt_write_output(self.ctx, str(path).encode(), int(flip_y)), "write_output")
 
     def trace_closest(self, rays: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
         """ray_intersects.glsl's closest-hit test kernel fed via UpdateRays (gpu_loader.cpp:198-210)."""

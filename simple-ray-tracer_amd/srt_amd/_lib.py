@@ -97,6 +97,8 @@ _SIGS = {
     "srt_alloc_images": (C.c_int, [P]),
     "srt_read_accum": (C.c_int, [P, P, C.c_size_t]),
     "srt_read_output": (C.c_int, [P, P, C.c_size_t]),
+    "srt_image_write": (C.c_int, [C.c_char_p, P, C.c_int, C.c_int, C.c_int]),
+    "srt_write_output": (C.c_int, [P, C.c_char_p, C.c_int]),
     "srt_write_accum": (C.c_int, [P, P, C.c_size_t]),
     "srt_image_pointers": (C.c_int, [P, C.POINTER(P), C.POINTER(P)]),
     "srt_set_image_buffers": (C.c_int, [P, P, P]),

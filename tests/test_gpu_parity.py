@@ -237,3 +237,19 @@ def test_cpp_api_program():
                     "-o", str(exe), "-L", str(PKG), "-lsrt_amd", f"-Wl,-rpath,{PKG}"], check=True)
     res = subprocess.run([str(exe), str(OBJECTS) + "/"], capture_output=True, text=True, timeout=120)
     assert res.returncode == 0 and res.stdout.startswith("OK"), res.stdout + res.stderr
+
+
+def test_save_image_matches_output(rubik, tmp_path):
+    """Output stage on a rendered frame: the PNG holds image0's bytes, top row first."""
+    from test_output_stage import _read_png
+
+    setup = R.make_setup(48, 40, show_model=True, models=[rubik])
+    r = R.Renderer(setup)
+    try:
+        r.render(2)
+        r.finish()
+        out = r.output()
+        r.compute.save_image(tmp_path / "frame.png")
+    finally:
+        r.close()
+    assert (_read_png(tmp_path / "frame.png") == out[::-1]).all()
