@@ -8,6 +8,8 @@
 //   src/asset_utils/gpu_loader.cpp:63-133      (UploadModelDataToGPU flattening)
 // All float arithmetic is plain IEEE fp32 in source order (the reference is
 // built by g++ for x86-64 without -march, so SSE and no FMA contraction).
+#include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cmath>
 #include <cstdio>
@@ -16,6 +18,7 @@
 #include <fstream>
 #include <limits>
 #include <sstream>
+#include <thread>
 #include <unordered_map>
 #include <zlib.h>
 
@@ -169,59 +172,77 @@ void ParseMTL(const std::string& folder, const std::string& file_name, std::vect
 // ---------------------------------------------------------------------------
 // BVH (bvh.h:40-148) over triangles, with model_loader.cpp:333-352 centre/bounds
 // ---------------------------------------------------------------------------
+// Runs body(i) for i in [0, n) on `threads` threads (dynamic, one index at a time).
+template <class F>
+void ParallelFor(size_t n, int threads, F body) {
+  if (threads <= 1 || n <= 1) {
+    for (size_t i = 0; i < n; ++i) body(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> pool;
+  const int t = (int)std::min<size_t>((size_t)threads, n);
+  for (int k = 0; k < t; ++k)
+    pool.emplace_back([&] {
+      for (size_t i; (i = next.fetch_add(1)) < n;) body(i);
+    });
+  for (auto& th : pool) th.join();
+}
+
+// bvh.h:40-148.  The reference builds recursively: a node that splits gets its
+// child pair at the next free index (pre-order), then its left subtree is
+// built completely, then its right.  So every subtree's pairs occupy one
+// contiguous block of indices, and the tree can be built in parallel with the
+// same bits: the top levels are split level by level (nodes of a level in
+// parallel: their primitive ranges are disjoint), the subtrees below are built
+// in parallel with local pre-order numbering, and one pre-order walk then gives
+// every block its global offset.  BuildBVH uses it above kParallelMinPrims
+// primitives (SRT_BVH_THREADS, default min(16, hardware threads); 1 = serial).
 class BvhBuilder {
  public:
-  BvhBuilder(Model* m) : m_(m) {}
+  BvhBuilder(Model* m, int threads) : m_(m), threads_(threads) {}
 
   void Build() {
     const size_t n = m_->prims.size();
     idx_.resize(n);
-    for (size_t i = 0; i < n; ++i) idx_[i] = static_cast<uint32_t>(i);
     centers_.resize(n);
     bmin_.resize(n);
     bmax_.resize(n);
-    for (size_t i = 0; i < n; ++i) {
-      const Triangle& t = m_->prims[i];
-      const Vec3 p0 = Pos(t.vertex_idxs[0]), p1 = Pos(t.vertex_idxs[1]), p2 = Pos(t.vertex_idxs[2]);
-      // (p0 + p1 + p2) / 3.0f
-      centers_[i] = Vec3((p0.x + p1.x + p2.x) / 3.0f, (p0.y + p1.y + p2.y) / 3.0f, (p0.z + p1.z + p2.z) / 3.0f);
-      Vec3 lo = vmin(vmin(p0, p1), p2);
-      Vec3 hi = vmax(vmax(p0, p1), p2);
-      bmin_[i] = lo;
-      bmax_[i] = hi;
-    }
-    nodes_.assign(n == 0 ? 1 : 2 * n - 1, BVHNode());
-    next_ = 1;
-    BVHNode& root = nodes_[0];
+    const size_t chunk = 1 << 16;
+    ParallelFor((n + chunk - 1) / chunk, threads_, [&](size_t c) {
+      for (size_t i = c * chunk; i < std::min(n, (c + 1) * chunk); ++i) {
+        idx_[i] = static_cast<uint32_t>(i);
+        const Triangle& t = m_->prims[i];
+        const Vec3 p0 = Pos(t.vertex_idxs[0]), p1 = Pos(t.vertex_idxs[1]), p2 = Pos(t.vertex_idxs[2]);
+        // (p0 + p1 + p2) / 3.0f
+        centers_[i] = Vec3((p0.x + p1.x + p2.x) / 3.0f, (p0.y + p1.y + p2.y) / 3.0f, (p0.z + p1.z + p2.z) / 3.0f);
+        bmin_[i] = vmin(vmin(p0, p1), p2);
+        bmax_[i] = vmax(vmax(p0, p1), p2);
+      }
+    });
+    BVHNode root;
     root.first_child = 0;
     root.first_prim_index = 0;
     root.prim_count = static_cast<uint32_t>(n);
-    UpdateBounds(0);
-    // iterative DFS that visits nodes in the recursive order (left, then right)
-    struct Item { uint32_t node; uint32_t depth; };
-    std::vector<Item> stack{{0, 0}};
+    UpdateBounds(&root);
     uint32_t max_depth = 0, leaves = 0;
-    while (!stack.empty()) {
-      Item it = stack.back();
-      stack.pop_back();
-      if (it.depth > max_depth) max_depth = it.depth;
-      uint32_t l = 0;
-      if (Subdivide(it.node, &l)) {
-        stack.push_back({l + 1, it.depth + 1});
-        stack.push_back({l, it.depth + 1});
-      } else {
-        ++leaves;
-      }
+    std::vector<BVHNode> nodes;
+    if (threads_ <= 1 || n < kParallelMinPrims) {
+      BuildSubtree(root, &nodes, &max_depth, &leaves);
+    } else {
+      BuildParallel(root, &nodes, &max_depth, &leaves);
     }
-    nodes_.resize(next_);
-    std::vector<Triangle> np;
-    np.reserve(n);
-    for (uint32_t i : idx_) np.push_back(m_->prims[i]);
+    std::vector<Triangle> np(n);
+    ParallelFor((n + chunk - 1) / chunk, threads_, [&](size_t c) {
+      for (size_t i = c * chunk; i < std::min(n, (c + 1) * chunk); ++i) np[i] = m_->prims[idx_[i]];
+    });
     m_->prims = std::move(np);
-    m_->nodes = std::move(nodes_);
+    m_->nodes = std::move(nodes);
     m_->max_depth = max_depth;
     m_->leaves = leaves;
   }
+
+  static constexpr size_t kParallelMinPrims = 65536;
 
  private:
   Vec3 Pos(uint32_t v) const {
@@ -230,31 +251,30 @@ class BvhBuilder {
   }
 
   // bvh.h:80-96
-  void UpdateBounds(uint32_t ni) {
-    BVHNode& node = nodes_[ni];
-    node.min_bounds = Vec3(std::numeric_limits<float>::max(), std::numeric_limits<float>::max(),
-                           std::numeric_limits<float>::max());
-    node.max_bounds = Vec3(std::numeric_limits<float>::lowest(), std::numeric_limits<float>::lowest(),
-                           std::numeric_limits<float>::lowest());
-    for (uint32_t i = 0; i < node.prim_count; ++i) {
-      const uint32_t p = idx_[node.first_prim_index + i];
-      node.min_bounds = vmin(node.min_bounds, bmin_[p]);
-      node.max_bounds = vmax(node.max_bounds, bmax_[p]);
+  void UpdateBounds(BVHNode* node) const {
+    node->min_bounds = Vec3(std::numeric_limits<float>::max(), std::numeric_limits<float>::max(),
+                            std::numeric_limits<float>::max());
+    node->max_bounds = Vec3(std::numeric_limits<float>::lowest(), std::numeric_limits<float>::lowest(),
+                            std::numeric_limits<float>::lowest());
+    for (uint32_t i = 0; i < node->prim_count; ++i) {
+      const uint32_t p = idx_[node->first_prim_index + i];
+      node->min_bounds = vmin(node->min_bounds, bmin_[p]);
+      node->max_bounds = vmax(node->max_bounds, bmax_[p]);
     }
   }
 
-  // bvh.h:98-148 (children are expanded by the caller, left first)
-  bool Subdivide(uint32_t ni, uint32_t* left_out) {
-    BVHNode& node = nodes_[ni];
-    if (node.prim_count <= 2) return false;
-    const Vec3 extent(node.max_bounds.x - node.min_bounds.x, node.max_bounds.y - node.min_bounds.y,
-                      node.max_bounds.z - node.min_bounds.z);
+  // bvh.h:98-148: partitions the node's range of idx_ and fills its children
+  // (first_child is left to the caller); false when the node stays a leaf
+  bool Split(BVHNode* node, BVHNode* left, BVHNode* right) {
+    if (node->prim_count <= 2) return false;
+    const Vec3 extent(node->max_bounds.x - node->min_bounds.x, node->max_bounds.y - node->min_bounds.y,
+                      node->max_bounds.z - node->min_bounds.z);
     int axis = 0;
     if (extent.y > extent.x) axis = 1;
     if (extent.z > extent[axis]) axis = 2;
-    const float split = node.min_bounds[axis] + extent[axis] * 0.5f;
-    uint32_t i = node.first_prim_index;
-    uint32_t j = i + node.prim_count - 1;
+    const float split = node->min_bounds[axis] + extent[axis] * 0.5f;
+    uint32_t i = node->first_prim_index;
+    uint32_t j = i + node->prim_count - 1;
     while (i <= j && j != static_cast<uint32_t>(-1)) {
       if (centers_[idx_[i]][axis] < split) {
         i++;
@@ -263,26 +283,151 @@ class BvhBuilder {
         j--;
       }
     }
-    const uint32_t left_count = i - node.first_prim_index;
-    if (left_count == 0 || left_count == node.prim_count) return false;
-    const uint32_t l = next_, r = next_ + 1;
-    node.first_child = l;
-    nodes_[l].first_prim_index = node.first_prim_index;
-    nodes_[l].prim_count = left_count;
-    nodes_[r].first_prim_index = i;
-    nodes_[r].prim_count = node.prim_count - left_count;
-    node.prim_count = 0;
-    next_ += 2;
-    UpdateBounds(l);
-    UpdateBounds(r);
-    *left_out = l;
+    const uint32_t left_count = i - node->first_prim_index;
+    if (left_count == 0 || left_count == node->prim_count) return false;
+    *left = BVHNode();
+    *right = BVHNode();
+    left->first_prim_index = node->first_prim_index;
+    left->prim_count = left_count;
+    right->first_prim_index = i;
+    right->prim_count = node->prim_count - left_count;
+    node->prim_count = 0;
+    UpdateBounds(left);
+    UpdateBounds(right);
     return true;
   }
 
+  // The subtree of `root` in the reference's order, numbered locally: out[0] =
+  // root, child pairs from 1 on in pre-order.  Depth and leaves are relative.
+  void BuildSubtree(const BVHNode& root, std::vector<BVHNode>* out, uint32_t* max_depth, uint32_t* leaves) {
+    out->assign(1, root);
+    struct Item { uint32_t node; uint32_t depth; };
+    std::vector<Item> stack{{0, 0}};
+    uint32_t md = 0, lv = 0;
+    while (!stack.empty()) {
+      const Item it = stack.back();
+      stack.pop_back();
+      if (it.depth > md) md = it.depth;
+      BVHNode l, r;
+      BVHNode node = (*out)[it.node];
+      if (Split(&node, &l, &r)) {
+        const uint32_t li = static_cast<uint32_t>(out->size());
+        node.first_child = li;
+        (*out)[it.node] = node;
+        out->push_back(l);
+        out->push_back(r);
+        stack.push_back({li + 1, it.depth + 1});
+        stack.push_back({li, it.depth + 1});
+      } else {
+        (*out)[it.node] = node;
+        ++lv;
+      }
+    }
+    *max_depth = md;
+    *leaves = lv;
+  }
+
+  struct TopNode {
+    BVHNode node;
+    int left = -1;      // index of the left child in top_ (right = left + 1)
+    int task = -1;      // subtree built by BuildSubtree
+    uint32_t depth = 0;
+  };
+
+  void BuildParallel(const BVHNode& root, std::vector<BVHNode>* out, uint32_t* max_depth, uint32_t* leaves) {
+    // 1. top levels, level by level, until there is enough independent work
+    top_.assign(1, TopNode{root, -1, -1, 0});
+    std::vector<int> level{0};
+    const size_t want = (size_t)threads_ * 8;
+    const uint32_t small = std::max<uint32_t>(4096, (uint32_t)(m_->prims.size() / (want * 4)));
+    while (!level.empty() && level.size() < want) {
+      std::vector<char> split(level.size(), 0);
+      std::vector<BVHNode> kids(2 * level.size());
+      ParallelFor(level.size(), threads_, [&](size_t k) {
+        TopNode& t = top_[level[k]];
+        if (t.node.prim_count <= small) return;  // left for the subtree stage
+        split[k] = Split(&t.node, &kids[2 * k], &kids[2 * k + 1]) ? 1 : 2;
+      });
+      std::vector<int> next;
+      for (size_t k = 0; k < level.size(); ++k) {
+        if (split[k] != 1) continue;  // 0: a subtree task, 2: a leaf
+        const int li = static_cast<int>(top_.size());
+        top_[level[k]].left = li;
+        const uint32_t d = top_[level[k]].depth + 1;
+        top_.push_back(TopNode{kids[2 * k], -1, -1, d});
+        top_.push_back(TopNode{kids[2 * k + 1], -1, -1, d});
+        next.push_back(li);
+        next.push_back(li + 1);
+      }
+      for (size_t k = 0; k < level.size(); ++k)
+        if (split[k] == 0) tasks_.push_back(level[k]);
+      level.swap(next);
+    }
+    for (int t : level) tasks_.push_back(t);
+    // 2. the subtrees, largest first
+    std::vector<int> order(tasks_.size());
+    for (size_t k = 0; k < order.size(); ++k) order[k] = (int)k;
+    std::sort(order.begin(), order.end(), [&](int a, int b) {
+      return top_[tasks_[a]].node.prim_count > top_[tasks_[b]].node.prim_count;
+    });
+    sub_.resize(tasks_.size());
+    sub_depth_.resize(tasks_.size());
+    sub_leaves_.resize(tasks_.size());
+    for (size_t k = 0; k < tasks_.size(); ++k) top_[tasks_[k]].task = (int)k;
+    ParallelFor(order.size(), threads_, [&](size_t q) {
+      const int k = order[q];
+      BuildSubtree(top_[tasks_[k]].node, &sub_[k], &sub_depth_[k], &sub_leaves_[k]);
+    });
+    // 3. global pre-order numbering
+    size_t total = 1;
+    for (const TopNode& t : top_)
+      if (t.left >= 0) total += 2;
+    for (const auto& v : sub_) total += v.size() - 1;
+    out->assign(total, BVHNode());
+    next_ = 1;
+    *max_depth = 0;
+    *leaves = 0;
+    Emit(0, 0, out, max_depth, leaves);
+  }
+
+  void Emit(int ti, uint32_t g, std::vector<BVHNode>* out, uint32_t* max_depth, uint32_t* leaves) {
+    const TopNode& t = top_[ti];
+    if (t.task >= 0) {
+      const std::vector<BVHNode>& loc = sub_[t.task];
+      const uint32_t base = next_;  // local index k >= 1 -> base + k - 1
+      next_ += static_cast<uint32_t>(loc.size() - 1);
+      auto remap = [&](BVHNode n) {
+        if (n.prim_count == 0) n.first_child = base + n.first_child - 1;
+        return n;
+      };
+      (*out)[g] = remap(loc[0]);
+      for (size_t k = 1; k < loc.size(); ++k) (*out)[base + k - 1] = remap(loc[k]);
+      *max_depth = std::max(*max_depth, t.depth + sub_depth_[t.task]);
+      *leaves += sub_leaves_[t.task];
+    } else if (t.left >= 0) {
+      const uint32_t pair = next_;
+      next_ += 2;
+      BVHNode n = t.node;
+      n.first_child = pair;
+      (*out)[g] = n;
+      *max_depth = std::max(*max_depth, t.depth);
+      Emit(t.left, pair, out, max_depth, leaves);
+      Emit(t.left + 1, pair + 1, out, max_depth, leaves);
+    } else {
+      (*out)[g] = t.node;
+      *max_depth = std::max(*max_depth, t.depth);
+      ++*leaves;
+    }
+  }
+
   Model* m_;
+  int threads_;
   std::vector<uint32_t> idx_;
   std::vector<Vec3> centers_, bmin_, bmax_;
-  std::vector<BVHNode> nodes_;
+  std::vector<TopNode> top_;
+  std::vector<int> tasks_;
+  std::vector<std::vector<BVHNode>> sub_;
+  std::vector<uint32_t> sub_depth_, sub_leaves_;
   uint32_t next_ = 0;
 };
 
@@ -400,7 +545,12 @@ bool DecodeTextureCornerAlbedo(const std::string& path, Vec3* out, std::string* 
   return true;
 }
 
-void BuildBVH(Model* m) { BvhBuilder(m).Build(); }
+int BvhThreads() {
+  if (const char* e = std::getenv("SRT_BVH_THREADS")) return std::max(1, std::atoi(e));
+  return (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
+void BuildBVH(Model* m) { BvhBuilder(m, BvhThreads()).Build(); }
 
 // model_loader.cpp:20-32 + 280-365
 std::unique_ptr<Model> LoadObjectFile(const std::string& obj_path, std::string* err) {

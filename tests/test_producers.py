@@ -215,3 +215,22 @@ def test_texture_corner_albedo(tmp_path):
 def test_missing_obj_raises(tmp_path):
     with pytest.raises(S.SrtError):
         S.load_obj(tmp_path / "nope.obj")
+
+
+@pytest.mark.parametrize("n_tris", [70_000, 300_000])
+def test_parallel_bvh_builder_is_bit_identical(monkeypatch, n_tris):
+    """SURVEY.md 8f item 1: the parallel builder (csrc/scene.cpp BvhBuilder::BuildParallel) reproduces the
+    reference's serial build (bvh.h:98-148) node for node and in primitive order."""
+    import hashlib
+
+    from srt_amd import render as R
+
+    tri = R.synthetic_triangles(n_tris, seed=11)
+    digests = []
+    for threads in ("1", "8"):
+        monkeypatch.setenv("SRT_BVH_THREADS", threads)
+        m = S.model_from_triangles(tri)
+        sc = S.Scene.from_models([m])
+        digests.append((hashlib.sha256(sc.nodes.tobytes()).hexdigest(), hashlib.sha256(sc.tris.tobytes()).hexdigest(),
+                        m.info()))
+    assert digests[0] == digests[1]
