@@ -343,6 +343,33 @@ __device__ __forceinline__ bool tri_accept(f3 o, f3 d, float4 A, float4 B, float
   return !parallel & !((u < 0.0f) | (u > 1.0f)) & !((v < 0.0f) | (u + v > 1.0f)) & (t > 0.00001f) & (t < dist);
 }
 
+// tri_accept split in two for the leaf step: the part up to the reciprocal
+// (true when |a| needs the division: recip_normal's fallback range), then the rest.
+struct TriPrep {
+  f3 v0, e1, e2, h;
+  float a, f;
+};
+__device__ __forceinline__ bool tri_prep(f3 d, float4 A, float4 B, float4 C, TriPrep& p) {
+  p.v0 = mk(A.x, A.y, A.z);
+  p.e1 = mk(A.w, B.x, B.y);
+  p.e2 = mk(B.z, B.w, C.x);
+  p.h = cross(d, p.e2);
+  p.a = dot(p.e1, p.h);
+  const float r = __builtin_amdgcn_rcpf(p.a);
+  p.f = __builtin_fmaf(__builtin_fmaf(-p.a, r, 1.0f), r, r);
+  return !(__builtin_fabsf(p.a) < 0x1p126f);
+}
+__device__ __forceinline__ bool tri_finish(f3 o, f3 d, const TriPrep& p, float dist, float& tout) {
+  const bool parallel = (p.a > -0.0001f) & (p.a < 0.0001f);
+  const f3 s = o - p.v0;
+  const float u = p.f * dot(s, p.h);
+  const f3 q = cross(s, p.e1);
+  const float v = p.f * dot(d, q);
+  const float t = p.f * dot(p.e2, q);
+  tout = t;
+  return !parallel & !((u < 0.0f) | (u > 1.0f)) & !((v < 0.0f) | (u + v > 1.0f)) & (t > 0.00001f) & (t < dist);
+}
+
 // Depth-first traversal in the reference's pop order (right child first).
 // Each child's box is tested once, when its parent is expanded; a child that
 // fails is never pushed (the running distance only shrinks, so it would fail
@@ -730,10 +757,20 @@ __device__ __forceinline__ void trav_leaf(const KParams& kp, Counters& c, Trav& 
   uint32_t hit = t.hit;
   bool stop = false;
   const float4* tp = tri_ptr<LDSM>(kp, t.ref);
+  // all triangles' loads and reciprocals first (one shared fallback branch),
+  // so the triangles' arithmetic overlaps; then the tests in order
+  TriPrep pr[kLeafTris];
+  bool slow = false;
+#pragma unroll
+  for (int k = 0; k < kLeafTris; ++k) slow |= tri_prep(t.d, tp[3 * k], tp[3 * k + 1], tp[3 * k + 2], pr[k]);
+  if (__builtin_expect(slow, 0)) {
+#pragma unroll
+    for (int k = 0; k < kLeafTris; ++k) pr[k].f = 1.0f / pr[k].a;
+  }
 #pragma unroll
   for (int k = 0; k < kLeafTris; ++k) {
     float tk;
-    const bool tk_ok = tri_accept(t.o, t.d, tp[3 * k], tp[3 * k + 1], tp[3 * k + 2], dist, tk);
+    const bool tk_ok = tri_finish(t.o, t.d, pr[k], dist, tk);
     const bool ak = k == 0 ? tk_ok : (((uint32_t)k < n) & !stop & tk_ok);  // a leaf holds >= 1 triangle
     dist = ak ? tk : dist;
     hit = ak ? t.ref + k : hit;
