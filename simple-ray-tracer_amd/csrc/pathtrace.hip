@@ -51,6 +51,7 @@ struct KParams {
   float4* accum;
   uint32_t* out;
   unsigned long long* stats;
+  unsigned long long* batch_ctr;  // next unclaimed 64-item batch of the launch (zeroed before it)
   int W, H, WH;
   int light_count;   // lightCount uniform (loop count)
   int light_records; // records in the light SSBO; index >= light_records reads zeros
@@ -723,6 +724,11 @@ constexpr char kStepPattern[] = SRT_STEP_PATTERN;
 #define SRT_SHORT_STACK 16
 #endif
 constexpr int kShortStack = SRT_SHORT_STACK;
+// consecutive 64-item batches a wave claims per atomic on the launch's batch counter
+#ifndef SRT_CLAIM
+#define SRT_CLAIM 4
+#endif
+constexpr int kClaim = SRT_CLAIM;
 static_assert((kShortStack & (kShortStack - 1)) == 0, "kShortStack must be a power of two");
 constexpr int kTriPad = 3;                // zero records past the triangle array (>= kLeafTris - 1)
 static_assert(kLeafTris >= 1 && kLeafTris - 1 <= kTriPad, "kLeafTris");
@@ -897,8 +903,6 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
     __syncthreads();
   }
   const int lane = tid & 63;
-  const int n_waves = (int)(gridDim.x * (blockDim.x >> 6));
-  const int wave_id = (int)(blockIdx.x * (blockDim.x >> 6)) + (tid >> 6);
   Lane ln;
   if constexpr (LDSM) {
     ln.stk = reinterpret_cast<uint32_t*>(g_smem + kp.stack_base_f4) + tid;
@@ -917,7 +921,16 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
   const int tiles_x = (kp.W + 7) >> 3;
   const int n_tiles = tiles_x * ((kp.local_rows + 7) >> 3);
   const long long n_batches = (long long)n_tiles * kp.nframes;
-  long long batch = wave_id;  // this wave's batches: wave_id, wave_id + n_waves, ...
+  // batches are claimed one at a time from a launch-wide counter, so waves
+  // that drew cheap tiles take more of them (no static-share tail).  The
+  // next batch is claimed one ahead: lane 0's atomic returns while the
+  // current batch is consumed, and is only read (broadcast) when needed.
+  // kClaim consecutive batches per claim.
+  unsigned long long claimed = 0;
+  if (lane == 0) claimed = atomicAdd(kp.batch_ctr, 1ull);
+  long long batch = (long long)__shfl(claimed, 0) * kClaim;
+  int claim_left = kClaim - 1;  // batches of the current claim after `batch`
+  if (lane == 0) claimed = atomicAdd(kp.batch_ctr, 1ull);
   int batch_next = 0;         // items of `batch` already handed out
 
   // per-lane sample / path / traversal state
@@ -1012,7 +1025,14 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
       const int taken = __popcll(idle) < avail ? __popcll(idle) : avail;
       batch_next += taken;
       if (batch_next == 64) {
-        batch += n_waves;
+        if (claim_left > 0) {
+          ++batch;
+          --claim_left;
+        } else {
+          batch = (long long)__shfl(claimed, 0) * kClaim;
+          claim_left = kClaim - 1;
+          if (lane == 0) claimed = atomicAdd(kp.batch_ctr, 1ull);
+        }
         batch_next = 0;
       }
     }
@@ -1392,6 +1412,8 @@ struct srt_context {
   float4* d_lbuf = nullptr;
   uint32_t* d_gstack = nullptr;  // global-scene mode traversal stacks
   size_t gstack_bytes = 0;
+  unsigned long long* d_batch_ctr = nullptr;  // one batch counter per chunk launch
+  int batch_ctr_cap = 0;
   size_t lbuf_bytes = 0;
   size_t lbuf_cap = (size_t)16 << 30;  // SRT_SAMPLE_BUFFER_MB
   int trav_frac16 = 8;                 // SRT_TRAV_FRAC16 (measured best on Rubik 1080p with 2-triangle leaf steps)
@@ -1605,6 +1627,14 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   HIP_OK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_TOTAL, c->stream));
   const int out_frames = kp.frame_first + kp.nframes - 1;
   const int nchunks = (kp.nframes + chunk - 1) / chunk;
+  if (nchunks > c->batch_ctr_cap) {
+    FreeDev(c->d_batch_ctr);
+    c->d_batch_ctr = nullptr;
+    c->batch_ctr_cap = 0;
+    HIP_OK(hipMalloc(&c->d_batch_ctr, sizeof(unsigned long long) * (size_t)nchunks));
+    c->batch_ctr_cap = nchunks;
+  }
+  HIP_OK(hipMemsetAsync(c->d_batch_ctr, 0, sizeof(unsigned long long) * (size_t)nchunks, c->stream));
   while ((int)c->ev.size() < 2 * nchunks) {
     hipEvent_t e;
     HIP_OK(hipEventCreate(&e));
@@ -1616,6 +1646,7 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
     kc.frame_first = kp.frame_first + f0;
     kc.nframes = std::min(chunk, kp.nframes - f0);
     kc.write_output = (f0 + chunk >= kp.nframes) ? kp.write_output : 0;
+    kc.batch_ctr = c->d_batch_ctr + f0 / chunk;
     int rc;
     HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
     // LDS mode: packed entries (lds_ok); global-scene mode: packed when indices fit 24 bits
@@ -1740,6 +1771,7 @@ int srt_destroy(srt_context* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   FreeDev(c->d_nodes); FreeDev(c->d_tris); FreeDev(c->d_mats); FreeDev(c->d_bvhs); FreeDev(c->d_lights);
   FreeDev(c->d_noise_xy); FreeDev(c->d_noise_u); FreeDev(c->d_stats); FreeDev(c->d_lbuf); FreeDev(c->d_gstack);
+  FreeDev(c->d_batch_ctr);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (!c->images_external) { FreeDev(c->d_accum); FreeDev(c->d_out); }
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
