@@ -688,8 +688,8 @@ __device__ __forceinline__ void flush_counters(const KParams& kp, const Counters
 //                     and stores each L_k (16 B) to an HBM sample buffer;
 //   accumulate_kernel adds them per pixel in frame order (bit-identical sum)
 //                     and writes the sRGB8 image.
-// sample_kernel is persistent: each wave walks its own round-robin share of
-// 64-item batches (an 8x8 tile of one frame); lanes whose path has ended take
+// sample_kernel is persistent: each wave claims 64-item batches (an 8x8 tile
+// of one frame) from a launch-wide counter; lanes whose path has ended take
 // the next items of the wave's batch with a ballot + prefix count, so lanes
 // stay busy regardless of per-pixel path cost.  Traversal is resumable: a
 // wave steps all traversing lanes until fewer than a threshold remain, then
@@ -920,15 +920,16 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
   const f3 center = mk(kp.cx, kp.cy, kp.cz);
   const int tiles_x = (kp.W + 7) >> 3;
   const int n_tiles = tiles_x * ((kp.local_rows + 7) >> 3);
-  const long long n_batches = (long long)n_tiles * kp.nframes;
+  const int n_batches = n_tiles * kp.nframes;  // < 2^31: the host bounds the frames per launch
   // batches are claimed one at a time from a launch-wide counter, so waves
   // that drew cheap tiles take more of them (no static-share tail).  The
   // next batch is claimed one ahead: lane 0's atomic returns while the
   // current batch is consumed, and is only read (broadcast) when needed.
   // kClaim consecutive batches per claim.
+  // `batch` and everything derived from it are wave-uniform (scalar registers).
   unsigned long long claimed = 0;
   if (lane == 0) claimed = atomicAdd(kp.batch_ctr, 1ull);
-  long long batch = (long long)__shfl(claimed, 0) * kClaim;
+  int batch = __builtin_amdgcn_readfirstlane((int)__shfl(claimed, 0)) * kClaim;
   int claim_left = kClaim - 1;  // batches of the current claim after `batch`
   if (lane == 0) claimed = atomicAdd(kp.batch_ctr, 1ull);
   int batch_next = 0;         // items of `batch` already handed out
@@ -983,14 +984,20 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
       if (idle == 0ull || batch >= n_batches) break;
       const int avail = 64 - batch_next;
       const int r = lane_rank(idle, lane);
+      // the batch's frame and 8x8 tile (wave-uniform integer divisions, once per batch)
+      const int frame_i = batch / n_tiles;
+      const int tile = batch - frame_i * n_tiles;
+      const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+      const int samp = (kp.frame_first + frame_i) % kp.WH;
+      // row band of the tile when bands are whole tiles (the default 8 rows)
+      const int band_u = (kp.band_rows & 7) == 0 ? ty / (kp.band_rows >> 3) : -1;
       if (!has_work && r < avail) {
         const int item = batch_next + r;
-        const int tile = (int)(batch % n_tiles);
-        const int frame_i = (int)(batch / n_tiles);
-        const int tx = tile % tiles_x, ty = tile / tiles_x;
         const int px = tx * 8 + (item & 7), ly = ty * 8 + (item >> 3);
         if (px < kp.ext_w && ly < kp.local_rows) {
-          const int band = ly / kp.band_rows;
+          int band;
+          if (band_u >= 0) band = band_u;
+          else band = ly / kp.band_rows;
           const int yy = (band * kp.nranks + kp.rank) * kp.band_rows + (ly - band * kp.band_rows);
           if (yy < kp.ext_h) {
             has_work = true;
@@ -1000,7 +1007,6 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
             fidx = frame_i;
             ln.base = gy * kp.H + x;
             // GetRay (raytrace_compute.glsl:78-90) with SampleSquare (raytrace_utils.glsl:10-17)
-            const int samp = (kp.frame_first + frame_i) % kp.WH;
             const float2 nz = kp.noise_xy[wrap_index(ln.base + samp, kp.WH)];
             bump<COUNT>(c, ST_RNGSQ);
             bump<COUNT>(c, ST_SAMPLES);
@@ -1029,7 +1035,7 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
           ++batch;
           --claim_left;
         } else {
-          batch = (long long)__shfl(claimed, 0) * kClaim;
+          batch = __builtin_amdgcn_readfirstlane((int)__shfl(claimed, 0)) * kClaim;
           claim_left = kClaim - 1;
           if (lane == 0) claimed = atomicAdd(kp.batch_ctr, 1ull);
         }
@@ -1613,7 +1619,11 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   }
   // sample buffer: as many frames per chunk as the buffer cap allows
   const size_t per_frame = (size_t)npx * sizeof(float4);
-  const int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)kp.nframes, c->lbuf_cap / per_frame));
+  // frames per launch: what the sample buffer holds, and n_tiles * frames < 2^31 (the kernel's batch index)
+  const size_t n_tiles = (size_t)((kp.W + 7) >> 3) * (size_t)((kp.local_rows + 7) >> 3);
+  const size_t max_frames = std::max<size_t>(1, (size_t)0x7FFFFFFF / std::max<size_t>(1, n_tiles) - 1);
+  const int chunk = (int)std::max<size_t>(
+      1, std::min<size_t>(std::min<size_t>((size_t)kp.nframes, max_frames), c->lbuf_cap / per_frame));
   const size_t need = per_frame * (size_t)chunk;
   if (need > c->lbuf_bytes) {
     FreeDev(c->d_lbuf);
