@@ -318,8 +318,7 @@ __device__ __forceinline__ void slot_read(const uint32_t* base, int stride, int 
 // wave needs it.  Callers must not use the result for denormal a (the
 // triangle test rejects |a| < 1e-4 before f matters).
 __device__ __forceinline__ float recip_normal(float a) {
-  const float r = __builtin_amdgcn_rcpf(a);
-  float f = __builtin_fmaf(__builtin_fmaf(-a, r, 1.0f), r, r);
+  float f = recip_newton(a);
   if (__builtin_expect(!(__builtin_fabsf(a) < 0x1p126f), 0)) f = 1.0f / a;
   return f;
 }
@@ -356,8 +355,7 @@ __device__ __forceinline__ bool tri_prep(f3 d, float4 A, float4 B, float4 C, Tri
   p.e2 = mk(B.z, B.w, C.x);
   p.h = cross(d, p.e2);
   p.a = dot(p.e1, p.h);
-  const float r = __builtin_amdgcn_rcpf(p.a);
-  p.f = __builtin_fmaf(__builtin_fmaf(-p.a, r, 1.0f), r, r);
+  p.f = recip_newton(p.a);
   return !(__builtin_fabsf(p.a) < 0x1p126f);
 }
 __device__ __forceinline__ bool tri_finish(f3 o, f3 d, const TriPrep& p, float dist, float& tout) {
@@ -387,7 +385,7 @@ __device__ uint32_t traverse(const KParams& kp, const Lane& ln, Counters& c, uin
   // (leaf: first triangle + remaining count; internal: index of its first
   // child, cnt == 0); kNone = nothing current, pop next.
   constexpr uint32_t kNone = 0xFFFFFFFFu;
-  const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const f3 inv = mk(recip_exact(d.x), recip_exact(d.y), recip_exact(d.z));
   uint32_t hit = kNone;
   const float4 rlo = node4<LDSM>(kp, 2 * root + 2), rhi = node4<LDSM>(kp, 2 * root + 3);
   bump<COUNT>(c, ST_NODES);
@@ -507,7 +505,7 @@ __device__ __forceinline__ int trace_spheres(f3 ro, f3 rd, float mn, float& dist
 __device__ __forceinline__ float light_falloff(f3 p, const LightRec& L) {
   const f3 d = L.pos - p;
   const float d2 = dot(d, d);
-  return 1.0f / ((0.01f * 0.01f) + d2);
+  return recip_exact((0.01f * 0.01f) + d2);
 }
 __device__ __forceinline__ f3 light_dir(const LightRec& L, f3 p) {
   const f3 ld = L.pos - p;
@@ -541,12 +539,12 @@ __device__ __forceinline__ float smithGAlpha(float alpha, float NdotS) {
   return NdotS / (fmx(0.0001f, alpha) * __builtin_sqrtf(1.0f - fmn(0.99999f, NdotS * NdotS)));
 }
 __device__ __forceinline__ float smithLambda(float a) {
-  return (-1.0f + __builtin_sqrtf(1.0f + (1.0f / fmx(0.001f, a * a)))) * 0.5f;
+  return (-1.0f + __builtin_sqrtf(1.0f + recip_exact(fmx(0.001f, a * a)))) * 0.5f;
 }
 __device__ __forceinline__ float smithG2(float alpha, float NdotL, float NdotV) {
   const float aL = smithGAlpha(alpha, NdotL);
   const float aV = smithGAlpha(alpha, NdotV);
-  return 1.0f / (1.0f + smithLambda(aL) + smithLambda(aV));
+  return recip_exact(1.0f + smithLambda(aL) + smithLambda(aV));
 }
 
 // brdf.glsl:200-224 SampleDirect up to the shadow factor: returns
@@ -740,7 +738,7 @@ __device__ __forceinline__ void trav_begin_bvh(const KParams& kp, Counters& c, T
   const srt_bvh_record& b = kp.bvhs[t.bi];
   t.o = xform(b.frame, ro, 1.0f);
   t.d = xform(b.frame, rd, 0.0f);
-  t.inv = mk(1.0f / t.d.x, 1.0f / t.d.y, 1.0f / t.d.z);
+  t.inv = mk(recip_exact(t.d.x), recip_exact(t.d.y), recip_exact(t.d.z));
   const uint32_t root = b.first_index;
   const float4 rlo = node4<LDSM>(kp, 2 * root + 2), rhi = node4<LDSM>(kp, 2 * root + 3);
   bump<COUNT>(c, ST_NODES);

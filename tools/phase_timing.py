@@ -1,4 +1,5 @@
-"""Diagnostic: phase split of sample_kernel (needs the SRT_PHASE_TIMING build via SRT_LIB_PATH)."""
+"""Diagnostic: phase split of sample_kernel (needs the SRT_PHASE_TIMING build via SRT_LIB_PATH; the
+per-sub-step lines need -DSRT_SUBSTEP_STATS too, whose atomics distort the timing)."""
 import ctypes as C, sys, pathlib, os
 ROOT = pathlib.Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd")); sys.path.insert(0, str(ROOT))
