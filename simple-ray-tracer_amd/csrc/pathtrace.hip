@@ -622,40 +622,52 @@ __device__ __forceinline__ f3 reflect3(f3 I, f3 N) { return I - N * (2.0f * dot(
 // brdf.glsl:239-277 SampleIndirectNew with its uniform draws r1 = U(p.xy),
 // r2 = U(p.yz) supplied (SampleDiffuse :60-74 and SampleSpecularHalfVec :81-99
 // both draw exactly these two numbers).
+// SampleIndirectNew (brdf.glsl:239-277).  The diffuse branch (SampleDiffuse +
+// its Fresnel weight from SampleSpecularHalfVec) and the specular branch
+// (SampleSpecularMicrofacet) share their basis, phi = 2*pi*r2 with its cos/sin
+// ((2*pi)*r2 and (r2*pi)*2 round identically: the factor 2 is exact), the GGX
+// half vector of (r1, r2) and one Fresnel evaluation, so lanes of a wave that
+// took different branches compute those once; every value is the reference's.
 __device__ bool sample_indirect(const Hit& hit, f3 Vv, int type, float r1, float r2, f3& dir, f3& weight) {
   const f3 N = hit.normal;
   if (dot(N, Vv) <= 0.0f) return false;
   const f3 specF0 = specularF0(hit.mat.albedo, hit.mat.metalness);
-  f3 nd;
+  const f3 B = perpendicular(N);
+  const f3 T = cross(B, N);
+  const float phi = 2.0f * 3.1415926535897f * r2;
+  const float cphi = cos_f(phi), sphi = sin_f(phi);
+  // SampleSpecularHalfVec(r1, r2, roughness, N) (brdf.glsl:81-99)
+  const float a2 = hit.mat.roughness * hit.mat.roughness;
+  const float cosT = __builtin_sqrtf(fmx(0.0f, (1.0f - r1) / ((a2 - 1.0f) * r1 + 1.0f)));
+  const float sinT = __builtin_sqrtf(fmx(0.0f, 1.0f - cosT * cosT));
+  const f3 Hs = ((T * (sinT * cphi)) + (B * (sinT * sphi))) + (N * cosT);
+  f3 nd, w0;
+  float fx;
   if (type == DIFFUSE_BRDF) {
-    const f3 B = perpendicular(N);
-    const f3 T = cross(B, N);
+    // SampleDiffuse (brdf.glsl:60-74)
     const float r = __builtin_sqrtf(__builtin_fabsf(r1));
-    const float phi = 2.0f * 3.1415926535897f * r2;
-    nd = ((T * (r * cos_f(phi))) + (B * (r * sin_f(phi)))) + (N * __builtin_sqrtf(__builtin_fabsf(1.0f - r1)));
-    weight = hit.mat.albedo * (1.0f - hit.mat.metalness);
-    const f3 H = specular_half(r1, r2, hit.mat.roughness, N);
-    const float VdotH = fmx(0.00001f, fmn(1.0f, dot(Vv, H)));
-    weight = weight * (mk(1.0f, 1.0f, 1.0f) - fresnelSchlickNew(specF0, shadowedF90(specF0), VdotH));
+    nd = ((T * (r * cphi)) + (B * (r * sphi))) + (N * __builtin_sqrtf(__builtin_fabsf(1.0f - r1)));
+    w0 = hit.mat.albedo * (1.0f - hit.mat.metalness);
+    fx = fmx(0.00001f, fmn(1.0f, dot(Vv, Hs)));  // VdotH
   } else {
     // brdf.glsl:102-132 SampleSpecularMicrofacet
     const float alpha = hit.mat.roughness * hit.mat.roughness;
     const float alphaSq = alpha * alpha;
-    f3 H;
+    f3 H = Hs;
     if (alpha == 0.0f) {
       const f3 Lt = reflect3(-Vv, N);
       H = normalize(-Vv + Lt);
-    } else {
-      H = specular_half(r1, r2, hit.mat.roughness, N);
     }
     const f3 L = reflect3(-Vv, H);
-    const float HdotL = fmx(0.00001f, fmn(1.0f, dot(H, L)));
+    fx = fmx(0.00001f, fmn(1.0f, dot(H, L)));  // HdotL
     const float NdotL = fmx(0.00001f, fmn(1.0f, dot(N, L)));
-    const f3 F = fresnelSchlickNew(specF0, shadowedF90(specF0), HdotL);
     const float N2 = NdotL * NdotL;
-    weight = F * (2.0f / (__builtin_sqrtf(((alphaSq * (1.0f - N2)) + N2) / N2) + 1.0f));
+    w0 = mk(2.0f / (__builtin_sqrtf(((alphaSq * (1.0f - N2)) + N2) / N2) + 1.0f), 0.0f, 0.0f);
     nd = L;
   }
+  const f3 F = fresnelSchlickNew(specF0, shadowedF90(specF0), fx);
+  if (type == DIFFUSE_BRDF) weight = w0 * (mk(1.0f, 1.0f, 1.0f) - F);
+  else weight = F * w0.x;
   if (luminance(weight) == 0.0f) return false;
   dir = normalize(nd);
   if (dot(N, dir) <= 0.0f) return false;
@@ -1181,13 +1193,10 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
           type = SPECULAR_BRDF;
         } else {
           const float bp = brdf_probability(rec.mat, Vv, rec.normal);
-          if (u_bp < bp) {
-            type = SPECULAR_BRDF;
-            T = T / bp;
-          } else {
-            type = DIFFUSE_BRDF;
-            T = T / (1.0f - bp);
-          }
+          // T / bp (specular) or T / (1 - bp) (diffuse): one division by the chosen divisor
+          const bool spec = u_bp < bp;
+          type = spec ? SPECULAR_BRDF : DIFFUSE_BRDF;
+          T = T / (spec ? bp : (1.0f - bp));
         }
         term = false;
         if (rr) {
