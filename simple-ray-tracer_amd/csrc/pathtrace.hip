@@ -502,16 +502,6 @@ __device__ __forceinline__ int trace_spheres(f3 ro, f3 rd, float mn, float& dist
   return best;
 }
 
-__device__ __forceinline__ float light_falloff(f3 p, const LightRec& L) {
-  const f3 d = L.pos - p;
-  const float d2 = dot(d, d);
-  return recip_exact((0.01f * 0.01f) + d2);
-}
-__device__ __forceinline__ f3 light_dir(const LightRec& L, f3 p) {
-  const f3 ld = L.pos - p;
-  return length(ld) > 0.0f ? normalize(ld) : ld;
-}
-
 template <bool COUNT>
 __device__ __forceinline__ LightRec load_light(const KParams& kp, Counters& c, int idx) {
   bump<COUNT>(c, ST_LIGHTS);
@@ -549,10 +539,9 @@ __device__ __forceinline__ float smithG2(float alpha, float NdotL, float NdotV) 
 
 // brdf.glsl:200-224 SampleDirect up to the shadow factor: returns
 // (ggxTerm + NdotL * albedo / pi) and the light term's unshadowed factors.
-__device__ f3 sample_direct_brdf(const Hit& hit, f3 Vv, const LightRec& L, float& li) {
-  const f3 Ld = light_dir(L, hit.p);
-  const f3 vl = Vv + Ld;
-  const f3 H = length(vl) > 0.0f ? normalize(vl) : vl;
+// Ld = getLightData's direction, H = its guarded half vector with V (computed
+// by the caller, shared with the shadow ray; li = intensity * falloff there too)
+__device__ f3 sample_direct_brdf(const Hit& hit, f3 Vv, f3 Ld, f3 H) {
   const f3 N = hit.normal;
   const float NdotL = sat(dot(N, Ld));
   const float NdotH = sat(dot(N, H));
@@ -562,8 +551,6 @@ __device__ f3 sample_direct_brdf(const Hit& hit, f3 Vv, const LightRec& L, float
   const float D = ggxD(NdotH, rough);
   const float G = ggxSchlickMasking(NdotL, NdotV, rough);
   const f3 F = schlickFresnel(hit.mat.specular, LdotH);
-  const float fo = light_falloff(hit.p, L);
-  li = L.intensity * fo;
   const f3 ggx = (F * (D * G)) / (4.0f * fmx(0.001f, NdotV));
   const f3 diff = (NdotL * hit.mat.albedo) / 3.1415926535897f;
   return ggx + diff;
@@ -571,9 +558,9 @@ __device__ f3 sample_direct_brdf(const Hit& hit, f3 Vv, const LightRec& L, float
 
 // brdf.glsl:226-237 SampleDirectNew (GetAllBRDFValues :173-198, EvalSpecular :139-145
 // with ggxNormalDistributionNew's arguments swapped as in the reference, EvalDiffuse :134-137)
-__device__ f3 sample_direct_new(const Hit& hit, f3 Vv, f3 L) {
+// H = normalize(L + Vv) (computed by the caller as normalize(Vv + L))
+__device__ f3 sample_direct_new(const Hit& hit, f3 Vv, f3 L, f3 H) {
   const f3 N = hit.normal;
-  const f3 H = normalize(L + Vv);
   const float NdotL = sat(dot(N, L));
   const float NdotV = sat(dot(N, Vv));
   const float LdotH = sat(dot(L, H));
@@ -1145,9 +1132,13 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
         bool selected = false;
         float lw = 0.0f;
         LightRec L;
+        f3 toL = mk(0.f, 0.f, 0.f);
+        float fo = 0.0f, d2L = 0.0f;
         if (n > 0) {
           L = load_light<COUNT>(kp, c, f2i(__builtin_rintf(r1 * (float)n)));
-          const float fo = light_falloff(p, L);
+          toL = L.pos - p;
+          d2L = dot(toL, toL);
+          fo = recip_exact((0.01f * 0.01f) + d2L);  // GetLightFalloff(p, L) (brdf.glsl:147-152)
           const float inten = L.intensity * fo;
           const float lpdf = luminance(mk(inten, inten, inten));
           const float ris = lpdf * (float)n;
@@ -1169,19 +1160,23 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
         f3 sdir = mk(0.f, 0.f, 0.f);
         float smax = 0.0f;
         if (selected) {
-          const f3 toL = L.pos - p;
-          sdir = normalize(toL);
-          smax = length(toL);
+          // shared by the shadow ray, getLightData and both direct-light BRDFs:
+          // length(toL), normalize(toL) = toL * (1 / length), light_dir = the
+          // normalized vector (toL itself when zero), the half vector of it and V
+          smax = __builtin_sqrtf(d2L);
+          sdir = toL * recip_exact(smax);
+          const f3 Ld = smax > 0.0f ? sdir : toL;
+          const f3 vl = Vv + Ld;
+          const float lvl = length(vl);
+          const f3 Hn = vl * recip_exact(lvl);  // normalize(vl)
           if (rec.mat.useSpec) {
-            float li_;
-            const f3 bd = sample_direct_brdf(rec, Vv, L, li_);
+            const float li_ = L.intensity * fo;
+            const f3 bd = sample_direct_brdf(rec, Vv, Ld, lvl > 0.0f ? Hn : vl);
             q1 = (T * (((1.0f * L.color) * li_) * bd)) * lw;
             q0 = (T * (((0.0f * L.color) * li_) * bd)) * lw;
           } else {
-            const f3 Ld = light_dir(L, p);
-            const float fo = light_falloff(p, L);
             const f3 lint = ((L.color * fo) * L.intensity) * lw;
-            const f3 tx = T * sample_direct_new(rec, Vv, Ld);
+            const f3 tx = T * sample_direct_new(rec, Vv, Ld, Hn);
             q1 = (tx * 1.0f) * lint;
             q0 = (tx * 0.0f) * lint;
           }
