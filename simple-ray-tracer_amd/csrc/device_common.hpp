@@ -1,0 +1,203 @@
+// device_common.hpp -- kernel parameters, launch statistics, per-lane context, RNG and small BRDF helpers
+// of the path-tracing kernels (included once, by pathtrace.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "pt_math.hpp"
+#include "srt_internal.hpp"
+
+namespace srt {
+using namespace dev;
+
+// ---------------------------------------------------------------------------
+// kernel parameters (kernarg segment -> scalar registers)
+// ---------------------------------------------------------------------------
+struct KParams {
+  const float4* nodes;   // node i at nodes[2*i + 2], nodes[2*i + 3]
+  const float4* tris;    // 3 float4 per triangle
+  const float4* mats;    // 2 float4 per material
+  const float4* lights;  // 2 float4 per light, light_count + 1 records
+  const srt_bvh_record* bvhs;
+  const float2* noise_xy;
+  const float* noise_u;
+  float4* accum;
+  uint32_t* out;
+  unsigned long long* stats;
+  unsigned long long* batch_ctr;  // next unclaimed 64-item batch of the launch (zeroed before it)
+  int W, H, WH;
+  int light_count;   // lightCount uniform (loop count)
+  int light_records; // records in the light SSBO; index >= light_records reads zeros
+  uint32_t bvh_count;
+  int show_model;
+  int max_depth;
+  int frame_first, nframes, write_output, reset;
+  int rank, nranks, band_rows, local_rows;
+  int ext_w, ext_h;
+  int stack_entries;
+  int nodes_f4, tris_f4;   // LDS-resident scene: sizes of the node / triangle arrays in float4
+  float4* lbuf;            // sample buffer: nframes x local_pixels radiance samples
+  int local_pixels;        // W * local_rows
+  int trav_frac16;         // resume shading when fewer than trav_frac16/16 of working lanes traverse
+  int stack_base_f4;       // first float4 of the per-lane stacks in dynamic LDS
+  uint32_t* gstack;        // global-scene mode: per-lane stacks in HBM, entry field k of lane g at gstack[k * stride + g]
+  int gstack_stride;       // lanes in the grid
+  float cx, cy, cz, p00x, p00y, p00z, dux, duy, duz, dvx, dvy, dvz;
+};
+
+// Dynamic LDS of the path-tracing kernels: [scene copy (LDS mode)] [per-lane stacks].
+extern __shared__ __attribute__((aligned(16))) float4 g_smem[];
+
+enum { ST_RAYS = 0, ST_NODES, ST_TRIS, ST_RNGU, ST_RNGSQ, ST_LIGHTS, ST_MATS, ST_SAMPLES, ST_OVERFLOW, ST_MAXSTACK,
+       ST_N, ST_CYC_REFILL = ST_N, ST_CYC_TRAV, ST_CYC_SHADE, ST_CYC_ITERS,
+       // lane occupancy of the traversal loop (summed popcounts per iteration) and of shading
+       ST_DBG_TITERS, ST_DBG_WORK, ST_DBG_TRAV, ST_DBG_LEAF, ST_DBG_INT, ST_DBG_SHADE,
+       // per traversal sub-step k < 16: lanes taking it (summed), waves executing it, lanes popping after it
+       ST_DBG_SUB, ST_TOTAL = ST_DBG_SUB + 48 };
+
+// Diagnostic build only (-DSRT_SUBSTEP_STATS): per-sub-step lane counts (global atomics, slow).
+#ifdef SRT_SUBSTEP_STATS
+__device__ __forceinline__ void dbg_count(unsigned long long* stats, int idx, bool cond, bool waves) {
+  const unsigned long long m = __ballot(cond);
+  if (m && (threadIdx.x & 63) == 0) {
+    atomicAdd(&stats[idx], (unsigned long long)__popcll(m));
+    if (waves) atomicAdd(&stats[idx + 1], 1ull);
+  }
+}
+#define DBG_COUNT(stats, idx, cond) dbg_count(stats, idx, cond, ((idx) - ST_DBG_SUB) % 3 == 0)
+#else
+#define DBG_COUNT(stats, idx, cond)
+#endif
+
+// Diagnostic build only (-DSRT_PHASE_TIMING): per-wave shader-clock stamps at the
+// phase boundaries of sample_kernel, summed into stats[ST_CYC_*].
+#ifdef SRT_PHASE_TIMING
+#define PHASE_STAMP(var) unsigned long long var = __builtin_amdgcn_s_memtime()
+#else
+#define PHASE_STAMP(var)
+#endif
+
+struct Counters {
+  uint32_t v[ST_N];
+};
+
+template <bool COUNT>
+__device__ __forceinline__ void bump(Counters& c, int k, uint32_t n = 1) {
+  if constexpr (COUNT) c.v[k] += n;
+}
+
+struct Mat {
+  f3 albedo, specular;
+  float roughness, metalness;
+  bool useSpec;
+};
+
+struct Hit {
+  bool hit;
+  f3 p, normal;
+  Mat mat;
+};
+
+struct LightRec {
+  f3 pos;
+  float intensity;
+  f3 color;
+};
+
+// raytrace_compute.glsl:299-364: five hard-coded spheres and their materials
+__device__ __forceinline__ void sphere_data(int i, f3& pos, float& radius, Mat& m) {
+  switch (i) {
+    case 0: pos = mk(1.8f, 0.0f, -2.0f); radius = 0.5f;   // blue (material4)
+      m = Mat{mk(0.2f, 0.4f, 1.0f), mk(0.8f, 0.8f, 0.9f), 0.01f, 0.9f, false}; break;
+    case 1: pos = mk(0.0f, -100.5f, -1.0f); radius = 100.0f;  // ground (material1)
+      m = Mat{mk(0.2f, 0.8f, 0.8f), mk(0.2f, 0.4f, 0.4f), 0.01f, 0.99f, false}; break;
+    case 2: pos = mk(0.55f, 0.0f, -2.0f); radius = 0.5f;  // green (material3)
+      m = Mat{mk(0.2f, 0.9f, 0.3f), mk(0.2f, 0.9f, 0.9f), 0.3f, 0.95f, true}; break;
+    case 3: pos = mk(-0.55f, 0.0f, -2.0f); radius = 0.5f;  // red (material2)
+      m = Mat{mk(0.8f, 0.3f, 0.3f), mk(0.9f, 0.7f, 0.7f), 0.1f, 0.5f, true}; break;
+    default: pos = mk(-1.8f, 0.0f, -2.0f); radius = 0.5f;  // yellow (material5)
+      m = Mat{mk(0.9f, 0.8f, 0.1f), mk(0.3f, 0.3f, 0.1f), 0.7f, 0.3f, false}; break;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// per-lane context
+// ---------------------------------------------------------------------------
+struct Lane {
+  int base;             // (y * Height) + x  (raytrace_utils.glsl:11-12,45-46)
+  uint32_t* stk;        // LDS stack: entry k field f at stk[(Fk+f) * stride] (global-scene mode: a ring of kShortStack)
+  int stride;
+  uint32_t* gstk;       // global-scene mode: the whole stack in HBM, same layout
+  int gstride;
+};
+
+// (a % m) for 0 <= a, 0 < m, with the common case a < 2m handled by one compare
+__device__ __forceinline__ int wrap_index(int a, int m) {
+  if (a >= m) a -= m;
+  if (a >= m) a %= m;  // only when Width < Height (index base y*Height + x can exceed W*H)
+  return a;
+}
+
+// raytrace_utils.glsl:28-30
+__device__ __forceinline__ float rand_float(float sx, float sy) {
+  const float d = sx * 12.9898f + sy * 78.233f;
+  return fractf(sin_f(d) * 43758.5453f);
+}
+
+// raytrace_utils.glsl:44-54 randFloatSampleUniform, split into the index and
+// the fetch so one bounce's independent draws are all in flight together.
+__device__ __forceinline__ int randU_index(const KParams& kp, const Lane& ln, float sx, float sy) {
+  const float r = rand_float(sx, sy) * (float)kp.W * (float)kp.H;
+  return wrap_index(ln.base + f2i(r), kp.WH);
+}
+template <bool COUNT>
+__device__ __forceinline__ float randU(const KParams& kp, const Lane& ln, Counters& c, float sx, float sy) {
+  bump<COUNT>(c, ST_RNGU);
+  return kp.noise_u[randU_index(kp, ln, sx, sy)];
+}
+
+__device__ __forceinline__ float luminance(f3 c) { return c.x * 0.2126f + c.y * 0.7152f + c.z * 0.0722f; }
+__device__ __forceinline__ f3 specularF0(f3 b, float m) {
+  const float om = 1.0f - m;
+  return mk(0.04f * om + b.x * m, 0.04f * om + b.y * m, 0.04f * om + b.z * m);
+}
+__device__ __forceinline__ f3 perpendicular(f3 u) {
+  const f3 a = mk(__builtin_fabsf(u.x), __builtin_fabsf(u.y), __builtin_fabsf(u.z));
+  const unsigned xm = ((a.x - a.y) < 0.0f && (a.x - a.z) < 0.0f) ? 1u : 0u;
+  const unsigned ym = (a.y - a.z) < 0.0f ? (1u ^ xm) : 0u;
+  const unsigned zm = 1u ^ (xm | ym);
+  return cross(u, mk((float)xm, (float)ym, (float)zm));
+}
+__device__ __forceinline__ float shadowedF90(f3 F0) { return fmn(1.0f, (1.0f / 0.04f) * luminance(F0)); }
+__device__ __forceinline__ f3 fresnelSchlickNew(f3 f0, float f90, float NdotS) {
+  const float p = pow5_f(1.0f - NdotS);
+  return f0 + mk(f90 - f0.x, f90 - f0.y, f90 - f0.z) * p;
+}
+__device__ __forceinline__ f3 schlickFresnel(f3 f0, float u) {
+  const float p = pow5_f(fmx(0.001f, 1.0f - u));
+  return f0 + (mk(1.0f, 1.0f, 1.0f) - f0) * p;
+}
+__device__ __forceinline__ float linearToSrgb(float c) {
+  if (c < 0.0031308f) return c * 12.92f;
+  return 1.055f * pow_f(c, 1.0f / 2.4f) - 0.055f;
+}
+__device__ __forceinline__ uint32_t to_unorm8(float x) {
+  if (x != x) return 0u;
+  return (uint32_t)__builtin_rintf(clampf(x, 0.0f, 1.0f) * 255.0f);
+}
+
+
+template <bool COUNT>
+__device__ __forceinline__ void flush_counters(const KParams& kp, const Counters& c) {
+  if constexpr (COUNT) {
+    for (int k = 0; k < ST_N; ++k) {
+      if (k == ST_MAXSTACK) {
+        atomicMax(&kp.stats[k], (unsigned long long)c.v[k]);
+      } else if (c.v[k]) {
+        atomicAdd(&kp.stats[k], (unsigned long long)c.v[k]);
+      }
+    }
+  }
+}
+
+}  // namespace srt

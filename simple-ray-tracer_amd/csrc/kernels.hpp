@@ -1,0 +1,499 @@
+// kernels.hpp -- the kernels: persistent sample_kernel, accumulate_kernel, reset_kernel,
+// closest_kernel (UpdateRays test path) and assemble_kernel (multi-GPU root).
+#pragma once
+
+#include "shading.hpp"
+#include "traversal.hpp"
+
+namespace srt {
+using namespace dev;
+
+// ---------------------------------------------------------------------------
+// the path-tracing kernels
+// ---------------------------------------------------------------------------
+// Work decomposition.  The reference accumulates one path sample per pixel
+// per frame: accum = (((accum + L_f0) + L_f0+1) + ...) (raytrace_compute.glsl:
+// 400-406).  Every sample L_k is independent (all randomness is a pure
+// function of pixel, frame and hit position), only the SUM is ordered.  So
+//   sample_kernel     computes samples (pixel, frame) in any order on any lane
+//                     and stores each L_k (16 B) to an HBM sample buffer;
+//   accumulate_kernel adds them per pixel in frame order (bit-identical sum)
+//                     and writes the sRGB8 image.
+// sample_kernel is persistent: each wave claims 64-item batches (an 8x8 tile
+// of one frame) from a launch-wide counter; lanes whose path has ended take
+// the next items of the wave's batch with a ballot + prefix count, so lanes
+// stay busy regardless of per-pixel path cost.  Traversal is resumable: a
+// wave steps all traversing lanes until fewer than a threshold remain, then
+// shades the lanes whose ray has returned (and refills them) while the rest
+// keep their traversal state (registers + LDS stack) for the next round.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
+  return __popcll(mask & ((1ull << lane) - 1ull));
+}
+
+#ifndef SRT_GLOBAL_WAVES
+#define SRT_GLOBAL_WAVES 4
+#endif
+// waves per SIMD the register allocation must allow: 4 (<= 128 VGPRs) in LDS
+// mode, where the 1024-thread block's LDS caps residency at 4 anyway;
+// SRT_GLOBAL_WAVES in global-scene mode, whose HBM latency wants more waves
+template <bool COUNT, bool LDSM, bool PACK, int BLOCK>
+__global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_kernel(KParams kp) {
+  const int tid = threadIdx.x;
+  if constexpr (LDSM) {  // the block copies the scene (nodes + triangles) into LDS once
+    const int total = kp.nodes_f4 + kp.tris_f4;
+    for (int i = tid; i < total; i += blockDim.x)
+      g_smem[i] = (i < kp.nodes_f4) ? kp.nodes[i] : kp.tris[i - kp.nodes_f4];
+    __syncthreads();
+  }
+  const int lane = tid & 63;
+  Lane ln;
+  if constexpr (LDSM) {
+    ln.stk = reinterpret_cast<uint32_t*>(g_smem + kp.stack_base_f4) + tid;
+    ln.stride = blockDim.x;
+  } else {  // the top kShortStack entries in an LDS ring, the rest in HBM (lane-interleaved, coalesced)
+    ln.stk = reinterpret_cast<uint32_t*>(g_smem) + tid;
+    ln.stride = BLOCK;
+    ln.gstk = kp.gstack + (size_t)blockIdx.x * BLOCK + tid;
+    ln.gstride = kp.gstack_stride;
+  }
+  ln.base = 0;
+  Counters c;
+  for (int k = 0; k < ST_N; ++k) c.v[k] = 0;
+
+  const f3 center = mk(kp.cx, kp.cy, kp.cz);
+  const int tiles_x = (kp.W + 7) >> 3;
+  const int n_tiles = tiles_x * ((kp.local_rows + 7) >> 3);
+  const int n_batches = n_tiles * kp.nframes;  // < 2^31: the host bounds the frames per launch
+  // batches are claimed one at a time from a launch-wide counter, so waves
+  // that drew cheap tiles take more of them (no static-share tail).  The
+  // next batch is claimed one ahead: lane 0's atomic returns while the
+  // current batch is consumed, and is only read (broadcast) when needed.
+  // kClaim consecutive batches per claim.
+  // `batch` and everything derived from it are wave-uniform (scalar registers).
+  unsigned long long claimed = 0;
+  if (lane == 0) claimed = atomicAdd(kp.batch_ctr, 1ull);
+  int batch = __builtin_amdgcn_readfirstlane((int)__shfl(claimed, 0)) * kClaim;
+  int claim_left = kClaim - 1;  // batches of the current claim after `batch`
+  if (lane == 0) claimed = atomicAdd(kp.batch_ctr, 1ull);
+  int batch_next = 0;         // items of `batch` already handed out
+
+  // per-lane sample / path / traversal state
+  bool has_work = false;
+  int x = 0, gy = 0, li = 0, fidx = 0;
+  f3 ro = mk(0.f, 0.f, 0.f), rd = mk(0.f, 0.f, 1.f), T, color, q0, q1, nd;
+  float tmax = 0.0f;
+  int depth = 0, randIndex = 0, hit_sphere = -1, bounces = 0;
+  bool shadow_phase = false, term = false;
+  Trav tr;
+  tr.active = false;
+  tr.start = false;
+  tr.hit = kNoneRef;
+
+  auto start_ray = [&]() {
+    tr.dist = tmax;
+    tr.hit = kNoneRef;
+    tr.bi = 0;
+    tr.active = true;
+    tr.start = false;
+    bump<COUNT>(c, ST_RAYS);
+    if (kp.show_model) {
+      trav_begin_bvh<COUNT, LDSM>(kp, c, tr, ro, rd);
+      if (tr.cnt == 0 && tr.ref == kNoneRef) {  // root box missed: next BVH, or done
+        if (kp.bvh_count > 1) tr.start = true, tr.bi = 1;
+        else tr.active = false;
+      }
+    } else {  // the five spheres are "traversed" in one go
+      float dist = tmax;
+      hit_sphere = trace_spheres(ro, rd, 0.001f, dist, shadow_phase);
+      tr.dist = dist;
+      tr.active = false;
+    }
+  };
+  auto finish_sample = [&]() {
+    color = color + T * mk(0.05f, 0.05f, 0.05f);  // skyColor, raytrace_compute.glsl:219,292
+    kp.lbuf[(size_t)fidx * (size_t)kp.local_pixels + (size_t)li] = make_float4(color.x, color.y, color.z, 0.0f);
+    has_work = false;
+  };
+
+#ifdef SRT_PHASE_TIMING
+  unsigned long long cyc_refill = 0, cyc_trav = 0, cyc_shade = 0, iters = 0;
+  unsigned long long d_titers = 0, d_work = 0, d_trav = 0, d_leaf = 0, d_int = 0, d_shade = 0;
+#endif
+  for (;;) {
+    PHASE_STAMP(t_a);
+    // ---- (A) idle lanes take the next items of the wave's batches ----
+    for (;;) {
+      const unsigned long long idle = __ballot(!has_work);
+      if (idle == 0ull || batch >= n_batches) break;
+      const int avail = 64 - batch_next;
+      const int r = lane_rank(idle, lane);
+      // the batch's frame and 8x8 tile (wave-uniform integer divisions, once per batch)
+      const int frame_i = batch / n_tiles;
+      const int tile = batch - frame_i * n_tiles;
+      const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+      const int samp = (kp.frame_first + frame_i) % kp.WH;
+      // row band of the tile when bands are whole tiles (the default 8 rows)
+      const int band_u = (kp.band_rows & 7) == 0 ? ty / (kp.band_rows >> 3) : -1;
+      if (!has_work && r < avail) {
+        const int item = batch_next + r;
+        const int px = tx * 8 + (item & 7), ly = ty * 8 + (item >> 3);
+        if (px < kp.ext_w && ly < kp.local_rows) {
+          int band;
+          if (band_u >= 0) band = band_u;
+          else band = ly / kp.band_rows;
+          const int yy = (band * kp.nranks + kp.rank) * kp.band_rows + (ly - band * kp.band_rows);
+          if (yy < kp.ext_h) {
+            has_work = true;
+            x = px;
+            gy = yy;
+            li = ly * kp.W + px;
+            fidx = frame_i;
+            ln.base = gy * kp.H + x;
+            // GetRay (raytrace_compute.glsl:78-90) with SampleSquare (raytrace_utils.glsl:10-17)
+            const float2 nz = kp.noise_xy[wrap_index(ln.base + samp, kp.WH)];
+            bump<COUNT>(c, ST_RNGSQ);
+            bump<COUNT>(c, ST_SAMPLES);
+            const f3 p00 = mk(kp.p00x, kp.p00y, kp.p00z);
+            const f3 du = mk(kp.dux, kp.duy, kp.duz);
+            const f3 dv = mk(kp.dvx, kp.dvy, kp.dvz);
+            const f3 ps = (p00 + du * ((float)x + (nz.x - 0.5f))) + dv * ((float)gy + (nz.y - 0.5f));
+            ro = center;
+            rd = ps - center;
+            tmax = __builtin_inff();
+            T = mk(1.0f, 1.0f, 1.0f);
+            color = mk(0.0f, 0.0f, 0.0f);
+            depth = kp.max_depth;
+            randIndex = 0;
+            bounces = 0;
+            shadow_phase = false;
+            term = false;
+            start_ray();
+          }
+        }
+      }
+      const int taken = __popcll(idle) < avail ? __popcll(idle) : avail;
+      batch_next += taken;
+      if (batch_next == 64) {
+        if (claim_left > 0) {
+          ++batch;
+          --claim_left;
+        } else {
+          batch = __builtin_amdgcn_readfirstlane((int)__shfl(claimed, 0)) * kClaim;
+          claim_left = kClaim - 1;
+          if (lane == 0) claimed = atomicAdd(kp.batch_ctr, 1ull);
+        }
+        batch_next = 0;
+      }
+    }
+    if (__ballot(has_work) == 0ull) break;
+    PHASE_STAMP(t_b);
+
+    // ---- (B) traverse until too few lanes are still traversing ----
+    if (kp.show_model) {
+      // has_work is fixed during traversal; trav_frac16 <= 16 makes
+      // n_trav * 16 < n_work * trav_frac16 imply n_trav < n_work
+      const int work_lim = __popcll(__ballot(has_work)) * kp.trav_frac16;
+      for (;;) {
+        const unsigned long long trav = __ballot(tr.active);
+        if (trav == 0ull) break;
+        if (__popcll(trav) * 16 < work_lim) break;
+#ifdef SRT_PHASE_TIMING
+        ++d_titers;
+        d_work += __popcll(__ballot(has_work));
+        d_trav += __popcll(trav);
+        d_leaf += __popcll(__ballot(tr.active && tr.cnt > 0));
+        d_int += __popcll(__ballot(tr.active && tr.cnt == 0 && tr.ref != kNoneRef));
+#endif
+        if (tr.active) trav_step<COUNT, LDSM, PACK>(kp, ln, c, tr, ro, rd, shadow_phase);
+      }
+    }
+
+    PHASE_STAMP(t_c);
+#ifdef SRT_PHASE_TIMING
+    d_shade += __popcll(__ballot(has_work && !tr.active));
+#endif
+    // ---- (C) lanes whose ray returned: shade (GetRayColor's loop body) ----
+    if (has_work && !tr.active) {
+      const bool hit = kp.show_model ? (tr.hit != kNoneRef) : (hit_sphere >= 0);
+      const float dist = tr.dist;
+      if (shadow_phase) {  // CheckLightOccluded returned: this bounce's direct light
+        color = color + (hit ? q0 : q1);
+        if (term) {
+          finish_sample();
+        } else {
+          rd = nd;  // the bounce ray starts at the same hit point as the shadow ray
+          tmax = __builtin_inff();
+          shadow_phase = false;
+          start_ray();
+        }
+      } else if (!hit) {
+        finish_sample();
+      } else {
+        // ---- hit record (CheckHit) ----
+        Hit rec;
+        rec.hit = true;
+        if (kp.show_model) {
+          rec.p = (dist * rd) + ro;
+          const uint32_t ht = tr.hit;
+          const float4 A = tri4<LDSM>(kp, 3 * ht), B = tri4<LDSM>(kp, 3 * ht + 1), C = tri4<LDSM>(kp, 3 * ht + 2);
+          rec.normal = normalize(cross(mk(A.w, B.x, B.y), mk(B.z, B.w, C.x)));
+          const uint32_t mi = __float_as_uint(C.y);
+          const float4 m0 = kp.mats[2 * mi], m1 = kp.mats[2 * mi + 1];
+          bump<COUNT>(c, ST_MATS);
+          rec.mat.albedo = mk(m0.x, m0.y, m0.z);
+          rec.mat.roughness = m0.w;
+          rec.mat.specular = mk(m1.x, m1.y, m1.z);
+          rec.mat.metalness = 0.1f;
+          rec.mat.useSpec = true;
+        } else {
+          f3 pos; float radius;
+          sphere_data(hit_sphere, pos, radius, rec.mat);
+          rec.p = ro + rd * dist;
+          const f3 outward = (rec.p - pos) / radius;   // SetFaceNormal (raytrace_utils.glsl:23-26)
+          rec.normal = (dot(rd, outward) < 0.0f) ? outward : -outward;
+        }
+        const f3 p = rec.p;
+        const f3 Vv = -rd;
+
+        // ---- this bounce's independent uniform draws, fetched together ----
+        const int n = kp.light_count;
+        const bool fixed_spec = (rec.mat.metalness == 1.0f && rec.mat.roughness == 0.0f);
+        const int i_r1 = randU_index(kp, ln, p.x, p.y);             // light index; SampleDiffuse r1
+        const int i_r2 = randU_index(kp, ln, p.y, p.z);             // SampleDiffuse r2
+        const int i_sel = randU_index(kp, ln, p.y + 0.0f, p.z + 0.0f);
+        const int i_bp = randU_index(kp, ln, p.x + (float)depth, p.y + (float)depth);
+        const bool rr = depth <= 0;
+        const int i_rr = rr ? randU_index(kp, ln, p.x + (float)randIndex, p.y + (float)randIndex) : 0;
+        const float r1 = kp.noise_u[i_r1];
+        const float r2 = kp.noise_u[i_r2];
+        const float u_sel0 = kp.noise_u[i_sel];
+        const float u_bp = kp.noise_u[i_bp];
+        const float u_rr = rr ? kp.noise_u[i_rr] : 1.0f;
+        if constexpr (COUNT) c.v[ST_RNGU] += 4 + (rr ? 1 : 0);
+
+        // ---- SampleLights (raytrace_compute.glsl:179-206) ----
+        // randLightIndex uses the same seed every iteration, so the light and its
+        // pdf are loop-invariant; after the first selection later iterations only
+        // re-select it, so their draws are skipped (the result is unchanged).
+        bool selected = false;
+        float lw = 0.0f;
+        LightRec L;
+        f3 toL = mk(0.f, 0.f, 0.f);
+        float fo = 0.0f, d2L = 0.0f;
+        if (n > 0) {
+          L = load_light<COUNT>(kp, c, f2i(__builtin_rintf(r1 * (float)n)));
+          toL = L.pos - p;
+          d2L = dot(toL, toL);
+          fo = recip_exact((0.01f * 0.01f) + d2L);  // GetLightFalloff(p, L) (brdf.glsl:147-152)
+          const float inten = L.intensity * fo;
+          const float lpdf = luminance(mk(inten, inten, inten));
+          const float ris = lpdf * (float)n;
+          float total = 0.0f, pdf = 0.0f;
+          for (int i = 0; i < n; ++i) {
+            total += ris;
+            if (!selected) {
+              const float r = (i == 0) ? u_sel0 : randU<COUNT>(kp, ln, c, p.y + (float)i, p.z + (float)i);
+              if (r < (ris / total)) {
+                pdf = lpdf;
+                selected = true;
+              }
+            }
+          }
+          lw = (total / (float)n) / fmx(0.001f, pdf);
+        }
+
+        // ---- direct light, both shadow outcomes (raytrace_compute.glsl:233-246) ----
+        f3 sdir = mk(0.f, 0.f, 0.f);
+        float smax = 0.0f;
+        if (selected) {
+          // shared by the shadow ray, getLightData and both direct-light BRDFs:
+          // length(toL), normalize(toL) = toL * (1 / length), light_dir = the
+          // normalized vector (toL itself when zero), the half vector of it and V
+          smax = __builtin_sqrtf(d2L);
+          sdir = toL * recip_exact(smax);
+          const f3 Ld = smax > 0.0f ? sdir : toL;
+          const f3 vl = Vv + Ld;
+          const float lvl = length(vl);
+          const f3 Hn = vl * recip_exact(lvl);  // normalize(vl)
+          if (rec.mat.useSpec) {
+            const float li_ = L.intensity * fo;
+            const f3 bd = sample_direct_brdf(rec, Vv, Ld, lvl > 0.0f ? Hn : vl);
+            q1 = (T * (((1.0f * L.color) * li_) * bd)) * lw;
+            q0 = (T * (((0.0f * L.color) * li_) * bd)) * lw;
+          } else {
+            const f3 lint = ((L.color * fo) * L.intensity) * lw;
+            const f3 tx = T * sample_direct_new(rec, Vv, Ld, Hn);
+            q1 = (tx * 1.0f) * lint;
+            q0 = (tx * 0.0f) * lint;
+          }
+        }
+
+        // ---- BRDF choice, Russian roulette, next direction (:248-285) ----
+        int type;
+        if (fixed_spec) {
+          type = SPECULAR_BRDF;
+        } else {
+          const float bp = brdf_probability(rec.mat, Vv, rec.normal);
+          // T / bp (specular) or T / (1 - bp) (diffuse): one division by the chosen divisor
+          const bool spec = u_bp < bp;
+          type = spec ? SPECULAR_BRDF : DIFFUSE_BRDF;
+          T = T / (spec ? bp : (1.0f - bp));
+        }
+        term = false;
+        if (rr) {
+          const float surv = clampf(luminance(T), 0.1f, 1.0f);
+          if (u_rr > surv) {
+            term = true;
+          } else {
+            T = T / surv;
+            randIndex++;
+          }
+        } else {
+          depth--;
+        }
+        if (!term) {
+          f3 dir, bw;
+          if (!sample_indirect(rec, Vv, type, r1, r2, dir, bw)) {
+            term = true;
+          } else {
+            T = T * bw;
+            nd = dir;
+          }
+        }
+
+        // The reference's loop has no depth cap (Russian roulette clamps the
+        // survival probability to >= 0.1).  A path still alive after 2^20
+        // bounces is cut (and counted) so a pathological scene cannot hang the GPU.
+        if (++bounces >= (1 << 20) && !term) {
+          term = true;
+          bump<COUNT>(c, ST_OVERFLOW);
+        }
+        ro = p;
+        if (selected) {  // trace CheckLightOccluded's ray next (t in (0.001, |light - p|))
+          rd = sdir;
+          tmax = smax;
+          shadow_phase = true;
+          start_ray();
+        } else if (term) {
+          finish_sample();
+        } else {
+          rd = nd;
+          tmax = __builtin_inff();
+          start_ray();
+        }
+      }
+    }
+#ifdef SRT_PHASE_TIMING
+    PHASE_STAMP(t_d);
+    cyc_refill += t_b - t_a;
+    cyc_trav += t_c - t_b;
+    cyc_shade += t_d - t_c;
+    ++iters;
+#endif
+  }
+#ifdef SRT_PHASE_TIMING
+  if (lane == 0) {
+    atomicAdd(&kp.stats[ST_CYC_REFILL], cyc_refill);
+    atomicAdd(&kp.stats[ST_CYC_TRAV], cyc_trav);
+    atomicAdd(&kp.stats[ST_CYC_SHADE], cyc_shade);
+    atomicAdd(&kp.stats[ST_CYC_ITERS], iters);
+    atomicAdd(&kp.stats[ST_DBG_TITERS], d_titers);
+    atomicAdd(&kp.stats[ST_DBG_WORK], d_work);
+    atomicAdd(&kp.stats[ST_DBG_TRAV], d_trav);
+    atomicAdd(&kp.stats[ST_DBG_LEAF], d_leaf);
+    atomicAdd(&kp.stats[ST_DBG_INT], d_int);
+    atomicAdd(&kp.stats[ST_DBG_SHADE], d_shade);
+  }
+#endif
+  flush_counters<COUNT>(kp, c);
+}
+
+// Ordered sum of the sample buffer into the accumulation image (raytrace_compute.glsl:
+// 404-406 for frames frame_first .. frame_first + nframes - 1) and the sRGB8
+// image for accumFrames = out_frames (:412-413).
+__global__ __launch_bounds__(256) void accumulate_kernel(KParams kp, int out_frames) {
+  const int li = blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= kp.local_pixels) return;
+  const int ly = li / kp.W, x = li - ly * kp.W;
+  const int band = ly / kp.band_rows;
+  const int gy = (band * kp.nranks + kp.rank) * kp.band_rows + (ly - band * kp.band_rows);
+  if (x >= kp.ext_w || gy >= kp.ext_h) return;
+  const float4 a0 = kp.accum[li];
+  f3 acc = mk(a0.x, a0.y, a0.z);
+  const float4* L = kp.lbuf + li;
+  for (int k = 0; k < kp.nframes; ++k) {
+    const float4 s = L[(size_t)k * (size_t)kp.local_pixels];
+    acc = acc + mk(s.x, s.y, s.z);
+  }
+  kp.accum[li] = make_float4(acc.x, acc.y, acc.z, 1.0f);
+  if (kp.write_output) {
+    const f3 o = acc / (float)out_frames;
+    const uint32_t r = to_unorm8(linearToSrgb(o.x)), g = to_unorm8(linearToSrgb(o.y)),
+                   b = to_unorm8(linearToSrgb(o.z));
+    kp.out[li] = r | (g << 8) | (b << 16) | (255u << 24);
+  }
+}
+
+// resetAccumBuffer (raytrace_compute.glsl:390-393)
+__global__ __launch_bounds__(256) void reset_kernel(KParams kp) {
+  const int li = blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= kp.local_pixels) return;
+  const int ly = li / kp.W, x = li - ly * kp.W;
+  const int band = ly / kp.band_rows;
+  const int gy = (band * kp.nranks + kp.rank) * kp.band_rows + (ly - band * kp.band_rows);
+  if (x >= kp.ext_w || gy >= kp.ext_h) return;
+  kp.accum[li] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+}
+
+// The closest-hit test kernel of ray_intersects.glsl:135-161.
+__global__ __launch_bounds__(256) void closest_kernel(KParams kp, const srt_ray* rays, uint32_t n, uint32_t* hits,
+                                                      float* tout) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Lane ln;
+  ln.base = 0;
+  ln.stk = reinterpret_cast<uint32_t*>(g_smem) + threadIdx.x;
+  ln.stride = blockDim.x;
+  Counters c;
+  for (int k = 0; k < ST_N; ++k) c.v[k] = 0;
+  const srt_ray r = rays[i];
+  const f3 o = mk(r.origin[0], r.origin[1], r.origin[2]);
+  const f3 d = mk(r.direction[0], r.direction[1], r.direction[2]);
+  float dist = r.intersection_distance;
+  uint32_t hit = 0xFFFFFFFFu;
+  for (uint32_t b = 0; b < kp.bvh_count; ++b) {
+    const srt_bvh_record& rec = kp.bvhs[b];
+    const uint32_t h = traverse<true, false>(kp, ln, c, rec.first_index, xform(rec.frame, o, 1.0f),
+                                      xform(rec.frame, d, 0.0f), dist, false);
+    if (h != 0xFFFFFFFFu) hit = h;
+  }
+  hits[i] = hit;
+  tout[i] = dist;
+  flush_counters<true>(kp, c);
+}
+
+// Root-side assembly after the multi-GPU gather: gathered[r] holds rank r's
+// packed local rows (bands b with b % nranks == r, `rows_pad` rows each);
+// writes the full-frame accumulation image and its sRGB8 display image
+// (raytrace_compute.glsl:412-413 with accumFrames = `frames`).
+__global__ __launch_bounds__(256) void assemble_kernel(const float4* gathered, int nranks, int rows_pad, int W, int H,
+                                                       int band_rows, int frames, float4* accum, uint32_t* out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)W * (size_t)H) return;
+  const int y = (int)(i / (size_t)W), x = (int)(i - (size_t)y * W);
+  const int band = y / band_rows;
+  const int r = band % nranks;
+  const int lband = band / nranks;
+  const int ly = lband * band_rows + (y - band * band_rows);
+  const float4 a = gathered[((size_t)r * rows_pad + ly) * W + x];
+  if (accum) accum[i] = a;
+  if (out) {
+    const float inv = (float)frames;
+    const f3 o = mk(a.x, a.y, a.z) / inv;
+    const uint32_t rr = to_unorm8(linearToSrgb(o.x)), g = to_unorm8(linearToSrgb(o.y)), b = to_unorm8(linearToSrgb(o.z));
+    out[i] = rr | (g << 8) | (b << 16) | (255u << 24);
+  }
+}
+
+}  // namespace srt

@@ -1,0 +1,206 @@
+// shading.hpp -- GetRayColor's shading: spheres, lights, the direct-light and indirect
+// BRDFs (shaders/brdf.glsl, raytrace_compute.glsl) in the arithmetic contract.
+#pragma once
+
+#include "device_common.hpp"
+
+namespace srt {
+using namespace dev;
+
+// raytrace_compute.glsl:93-120 SphereHit
+__device__ __forceinline__ bool sphere_hit(f3 ro, f3 rd, f3 pos, float radius, float mn, float mx, float& t) {
+  const f3 oc = pos - ro;
+  const float ld = length(rd);
+  const float a = ld * ld;
+  const float h = dot(rd, oc);
+  const float loc = length(oc);
+  const float cc = loc * loc - (radius * radius);
+  const float disc = h * h - a * cc;
+  if (disc < 0.0f) return false;
+  const float sq = __builtin_sqrtf(disc);
+  float root = (h - sq) / a;
+  if (!(mn < root && root < mx)) {
+    root = (h + sq) / a;
+    if (!(mn < root && root < mx)) return false;
+  }
+  t = root;
+  return true;
+}
+
+// CheckHit over the five spheres (raytrace_compute.glsl:132-141): index of the
+// closest sphere (dist updated) or, with `any`, of the first sphere hit; -1 if none.
+__device__ __forceinline__ int trace_spheres(f3 ro, f3 rd, float mn, float& dist, bool any) {
+  int best = -1;
+  for (int i = 0; i < 5; ++i) {
+    f3 pos; float radius; Mat m;
+    sphere_data(i, pos, radius, m);
+    float t;
+    if (sphere_hit(ro, rd, pos, radius, mn, dist, t)) {
+      best = i;
+      dist = t;
+      if (any) break;
+    }
+  }
+  return best;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ LightRec load_light(const KParams& kp, Counters& c, int idx) {
+  bump<COUNT>(c, ST_LIGHTS);
+  const int i = (idx >= 0 && idx < kp.light_records) ? idx : kp.light_records;  // zero record
+  const float4 a = kp.lights[2 * i], b = kp.lights[2 * i + 1];
+  return LightRec{mk(a.x, a.y, a.z), a.w, mk(b.x, b.y, b.z)};
+}
+
+__device__ __forceinline__ float ggxD(float NdotH, float rough) {
+  const float a2 = rough * rough;
+  const float d = ((NdotH * a2 - NdotH) * NdotH + 1.0f);
+  return a2 / fmx(0.001f, (d * d * 3.1415926535897f));
+}
+__device__ __forceinline__ float ggxDNew(float NdotH, float alphaSquared) {
+  const float b = ((alphaSquared - 1.0f) * NdotH * NdotH + 1.0f);
+  return alphaSquared / fmx(0.001f, (3.1415926535897f * b * b));
+}
+__device__ __forceinline__ float ggxSchlickMasking(float NdotL, float NdotV, float rough) {
+  const float k = rough * rough / 2.0f;
+  const float gv = NdotV / fmx(0.001f, (NdotV * (1.0f - k) + k));
+  const float gl = NdotL / fmx(0.001f, (NdotL * (1.0f - k) + k));
+  return __builtin_fabsf(gv * gl);
+}
+__device__ __forceinline__ float smithGAlpha(float alpha, float NdotS) {
+  return NdotS / (fmx(0.0001f, alpha) * __builtin_sqrtf(1.0f - fmn(0.99999f, NdotS * NdotS)));
+}
+__device__ __forceinline__ float smithLambda(float a) {
+  return (-1.0f + __builtin_sqrtf(1.0f + recip_exact(fmx(0.001f, a * a)))) * 0.5f;
+}
+__device__ __forceinline__ float smithG2(float alpha, float NdotL, float NdotV) {
+  const float aL = smithGAlpha(alpha, NdotL);
+  const float aV = smithGAlpha(alpha, NdotV);
+  return recip_exact(1.0f + smithLambda(aL) + smithLambda(aV));
+}
+
+// brdf.glsl:200-224 SampleDirect up to the shadow factor: returns
+// (ggxTerm + NdotL * albedo / pi) and the light term's unshadowed factors.
+// Ld = getLightData's direction, H = its guarded half vector with V (computed
+// by the caller, shared with the shadow ray; li = intensity * falloff there too)
+__device__ f3 sample_direct_brdf(const Hit& hit, f3 Vv, f3 Ld, f3 H) {
+  const f3 N = hit.normal;
+  const float NdotL = sat(dot(N, Ld));
+  const float NdotH = sat(dot(N, H));
+  const float LdotH = sat(dot(Ld, H));
+  const float NdotV = sat(dot(N, Vv));
+  const float rough = hit.mat.roughness;
+  const float D = ggxD(NdotH, rough);
+  const float G = ggxSchlickMasking(NdotL, NdotV, rough);
+  const f3 F = schlickFresnel(hit.mat.specular, LdotH);
+  const f3 ggx = (F * (D * G)) / (4.0f * fmx(0.001f, NdotV));
+  const f3 diff = (NdotL * hit.mat.albedo) / 3.1415926535897f;
+  return ggx + diff;
+}
+
+// brdf.glsl:226-237 SampleDirectNew (GetAllBRDFValues :173-198, EvalSpecular :139-145
+// with ggxNormalDistributionNew's arguments swapped as in the reference, EvalDiffuse :134-137)
+// H = normalize(L + Vv) (computed by the caller as normalize(Vv + L))
+__device__ f3 sample_direct_new(const Hit& hit, f3 Vv, f3 L, f3 H) {
+  const f3 N = hit.normal;
+  const float NdotL = sat(dot(N, L));
+  const float NdotV = sat(dot(N, Vv));
+  const float LdotH = sat(dot(L, H));
+  const float NdotH = sat(dot(N, H));
+  const f3 specF0 = specularF0(hit.mat.albedo, hit.mat.metalness);
+  const f3 diffRefl = hit.mat.albedo * (1.0f - hit.mat.metalness);
+  const float alpha = hit.mat.roughness * hit.mat.roughness;
+  const float alphaSq = alpha * alpha;
+  const f3 F = fresnelSchlickNew(specF0, shadowedF90(specF0), LdotH);
+  const float D = ggxDNew(fmx(0.00001f, alphaSq), NdotH);
+  const float G = smithG2(alpha, NdotL, NdotV);
+  const float denom = 4.0f * fmx(NdotL, 0.001f) * fmx(NdotV, 0.001f);
+  const f3 spec = (((F * G) * D) / fmx(denom, 0.001f)) * NdotL;
+  const float oneOverPi = 1.0f / 3.1415926535897f;
+  const f3 diff = diffRefl * (oneOverPi * NdotL);
+  return ((mk(1.0f, 1.0f, 1.0f) - F) * diff) + spec;
+}
+
+// brdf.glsl:279-288
+__device__ float brdf_probability(const Mat& m, f3 Vv, f3 N) {
+  const float sF0 = luminance(specularF0(m.albedo, m.metalness));
+  const float dR = luminance(m.albedo * (1.0f - m.metalness));
+  const f3 f0 = mk(sF0, sF0, sF0);
+  const float F = sat(luminance(fresnelSchlickNew(f0, shadowedF90(f0), fmx(0.0f, dot(Vv, N)))));
+  const float diffuse = dR * (1.0f - F);
+  const float p = (F / fmx(0.0001f, (F + diffuse)));
+  return clampf(p, 0.1f, 0.9f);
+}
+
+// brdf.glsl:81-99 SampleSpecularHalfVec given its two uniform draws
+__device__ __forceinline__ f3 specular_half(float rx, float ry, float rough, f3 N) {
+  const f3 B = perpendicular(N);
+  const f3 T = cross(B, N);
+  const float a2 = rough * rough;
+  const float cosT = __builtin_sqrtf(fmx(0.0f, (1.0f - rx) / ((a2 - 1.0f) * rx + 1.0f)));
+  const float sinT = __builtin_sqrtf(fmx(0.0f, 1.0f - cosT * cosT));
+  const float phi = ry * 3.1415926535897f * 2.0f;
+  return ((T * (sinT * cos_f(phi))) + (B * (sinT * sin_f(phi)))) + (N * cosT);
+}
+
+__device__ __forceinline__ f3 reflect3(f3 I, f3 N) { return I - N * (2.0f * dot(N, I)); }
+
+#define DIFFUSE_BRDF 1
+#define SPECULAR_BRDF 2
+
+// brdf.glsl:239-277 SampleIndirectNew with its uniform draws r1 = U(p.xy),
+// r2 = U(p.yz) supplied (SampleDiffuse :60-74 and SampleSpecularHalfVec :81-99
+// both draw exactly these two numbers).
+// SampleIndirectNew (brdf.glsl:239-277).  The diffuse branch (SampleDiffuse +
+// its Fresnel weight from SampleSpecularHalfVec) and the specular branch
+// (SampleSpecularMicrofacet) share their basis, phi = 2*pi*r2 with its cos/sin
+// ((2*pi)*r2 and (r2*pi)*2 round identically: the factor 2 is exact), the GGX
+// half vector of (r1, r2) and one Fresnel evaluation, so lanes of a wave that
+// took different branches compute those once; every value is the reference's.
+__device__ bool sample_indirect(const Hit& hit, f3 Vv, int type, float r1, float r2, f3& dir, f3& weight) {
+  const f3 N = hit.normal;
+  if (dot(N, Vv) <= 0.0f) return false;
+  const f3 specF0 = specularF0(hit.mat.albedo, hit.mat.metalness);
+  const f3 B = perpendicular(N);
+  const f3 T = cross(B, N);
+  const float phi = 2.0f * 3.1415926535897f * r2;
+  const float cphi = cos_f(phi), sphi = sin_f(phi);
+  // SampleSpecularHalfVec(r1, r2, roughness, N) (brdf.glsl:81-99)
+  const float a2 = hit.mat.roughness * hit.mat.roughness;
+  const float cosT = __builtin_sqrtf(fmx(0.0f, (1.0f - r1) / ((a2 - 1.0f) * r1 + 1.0f)));
+  const float sinT = __builtin_sqrtf(fmx(0.0f, 1.0f - cosT * cosT));
+  const f3 Hs = ((T * (sinT * cphi)) + (B * (sinT * sphi))) + (N * cosT);
+  f3 nd, w0;
+  float fx;
+  if (type == DIFFUSE_BRDF) {
+    // SampleDiffuse (brdf.glsl:60-74)
+    const float r = __builtin_sqrtf(__builtin_fabsf(r1));
+    nd = ((T * (r * cphi)) + (B * (r * sphi))) + (N * __builtin_sqrtf(__builtin_fabsf(1.0f - r1)));
+    w0 = hit.mat.albedo * (1.0f - hit.mat.metalness);
+    fx = fmx(0.00001f, fmn(1.0f, dot(Vv, Hs)));  // VdotH
+  } else {
+    // brdf.glsl:102-132 SampleSpecularMicrofacet
+    const float alpha = hit.mat.roughness * hit.mat.roughness;
+    const float alphaSq = alpha * alpha;
+    f3 H = Hs;
+    if (alpha == 0.0f) {
+      const f3 Lt = reflect3(-Vv, N);
+      H = normalize(-Vv + Lt);
+    }
+    const f3 L = reflect3(-Vv, H);
+    fx = fmx(0.00001f, fmn(1.0f, dot(H, L)));  // HdotL
+    const float NdotL = fmx(0.00001f, fmn(1.0f, dot(N, L)));
+    const float N2 = NdotL * NdotL;
+    w0 = mk(2.0f / (__builtin_sqrtf(((alphaSq * (1.0f - N2)) + N2) / N2) + 1.0f), 0.0f, 0.0f);
+    nd = L;
+  }
+  const f3 F = fresnelSchlickNew(specF0, shadowedF90(specF0), fx);
+  if (type == DIFFUSE_BRDF) weight = w0 * (mk(1.0f, 1.0f, 1.0f) - F);
+  else weight = F * w0.x;
+  if (luminance(weight) == 0.0f) return false;
+  dir = normalize(nd);
+  if (dot(N, dir) <= 0.0f) return false;
+  return true;
+}
+
+}  // namespace srt

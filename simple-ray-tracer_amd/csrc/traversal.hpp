@@ -1,0 +1,450 @@
+// traversal.hpp -- BVH traversal, order-exact: slab and Moller-Trumbore tests, scene
+// access (LDS copy or HBM), traversal stacks, the flat closest-hit walk and the
+// resumable step machine of sample_kernel.
+#pragma once
+
+#include "device_common.hpp"
+
+namespace srt {
+using namespace dev;
+
+// ---------------------------------------------------------------------------
+// BVH traversal (ray_intersects.glsl:49-133), order-exact
+// ---------------------------------------------------------------------------
+// IntersectsBox.  Hardware v_min/v_max (IEEE minNum/maxNum) give the same
+// value as GLSL min/max up to the sign of a zero result, and the result is
+// only ever compared (< dist, isinf), so every decision is unchanged.
+__device__ __forceinline__ float box_t(f3 o, f3 inv, float4 lo, float4 hi) {
+  const float t0x = (lo.x - o.x) * inv.x, t0y = (lo.y - o.y) * inv.y, t0z = (lo.z - o.z) * inv.z;
+  const float t1x = (hi.x - o.x) * inv.x, t1y = (hi.y - o.y) * inv.y, t1z = (hi.z - o.z) * inv.z;
+  const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t0x, t1x), __builtin_fminf(t0y, t1y)),
+                                   __builtin_fminf(t0z, t1z));
+  const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t0x, t1x), __builtin_fmaxf(t0y, t1y)),
+                                   __builtin_fmaxf(t0z, t1z));
+  return tn <= tf ? ((tn >= 0.0f) ? tn : tf) : __builtin_inff();
+}
+
+__device__ __forceinline__ bool box_ok(float b, float dist) { return b < dist && !isinf_f(b); }
+
+// LDS byte offsets are 32-bit: keep the address arithmetic in 32 bits.
+__device__ __forceinline__ float4 lds4(uint32_t byte_off) {
+  return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(g_smem) + byte_off);
+}
+template <bool LDSM>
+__device__ __forceinline__ float4 node4(const KParams& kp, uint32_t i) {
+  if constexpr (LDSM) return lds4(i << 4);
+  else return kp.nodes[i];
+}
+// the records of triangle `i` onwards (3 float4 per triangle)
+template <bool LDSM>
+__device__ __forceinline__ const float4* tri_ptr(const KParams& kp, uint32_t i) {
+  if constexpr (LDSM)
+    return reinterpret_cast<const float4*>(reinterpret_cast<const char*>(g_smem) + (((uint32_t)kp.nodes_f4 + 3 * i) << 4));
+  else return kp.tris + 3 * (size_t)i;
+}
+template <bool LDSM>
+__device__ __forceinline__ float4 tri4(const KParams& kp, uint32_t i) {
+  if constexpr (LDSM) return lds4(((uint32_t)kp.nodes_f4 + i) << 4);
+  else return kp.tris[i];
+}
+
+// Traversal stack entry: global mode 3 dwords (ref, count, t); LDS mode 2
+// dwords (ref | count << 24, t) -- LDS mode is only used for scenes whose
+// triangle / node indices fit 24 bits and leaves hold < 256 triangles.
+template <bool LDSM>
+__device__ __forceinline__ void stk_push(const Lane& ln, int sp, uint32_t ref, uint32_t cnt, float t) {
+  if constexpr (LDSM) {
+    ln.stk[(2 * sp + 0) * ln.stride] = ref | (cnt << 24);
+    ln.stk[(2 * sp + 1) * ln.stride] = __float_as_uint(t);
+  } else {
+    ln.stk[(3 * sp + 0) * ln.stride] = ref;
+    ln.stk[(3 * sp + 1) * ln.stride] = cnt;
+    ln.stk[(3 * sp + 2) * ln.stride] = __float_as_uint(t);
+  }
+}
+template <bool LDSM>
+__device__ __forceinline__ float stk_t(const Lane& ln, int sp) {
+  return __uint_as_float(ln.stk[((LDSM ? 2 : 3) * sp + (LDSM ? 1 : 2)) * ln.stride]);
+}
+template <bool LDSM>
+__device__ __forceinline__ void stk_ref(const Lane& ln, int sp, uint32_t& ref, uint32_t& cnt) {
+  if constexpr (LDSM) {
+    const uint32_t w = ln.stk[(2 * sp) * ln.stride];
+    ref = w & 0xFFFFFFu;
+    cnt = w >> 24;
+  } else {
+    ref = ln.stk[(3 * sp + 0) * ln.stride];
+    cnt = ln.stk[(3 * sp + 1) * ln.stride];
+  }
+}
+// Entry `slot` of a lane-interleaved stack area (LDS or HBM): field k of the
+// entry at base[(F * slot + k) * stride], F = 2 (PACK: ref | count << 24, t) or 3.
+template <bool PACK>
+__device__ __forceinline__ void slot_write(uint32_t* base, int stride, int slot, uint32_t ref, uint32_t cnt, float t) {
+  if constexpr (PACK) {
+    base[(2 * slot + 0) * stride] = ref | (cnt << 24);
+    base[(2 * slot + 1) * stride] = __float_as_uint(t);
+  } else {
+    base[(3 * slot + 0) * stride] = ref;
+    base[(3 * slot + 1) * stride] = cnt;
+    base[(3 * slot + 2) * stride] = __float_as_uint(t);
+  }
+}
+template <bool PACK>
+__device__ __forceinline__ void slot_read(const uint32_t* base, int stride, int slot, uint32_t& ref, uint32_t& cnt,
+                                          float& t) {
+  if constexpr (PACK) {
+    const uint32_t w = base[(2 * slot + 0) * stride];
+    ref = w & 0xFFFFFFu;
+    cnt = w >> 24;
+    t = __uint_as_float(base[(2 * slot + 1) * stride]);
+  } else {
+    ref = base[(3 * slot + 0) * stride];
+    cnt = base[(3 * slot + 1) * stride];
+    t = __uint_as_float(base[(3 * slot + 2) * stride]);
+  }
+}
+
+// 1.0f / a, correctly rounded, for every a that is not denormal.  v_rcp_f32
+// plus one FMA Newton step equals the correctly rounded quotient for every
+// 2^-126 <= |a| < 2^126 (all 2^32 inputs checked on gfx950:
+// tools/rcp_exhaustive.hip, tests/test_gpu_rcp.py); |a| >= 2^126, inf and NaN
+// take the full division on a branch that is skipped unless some lane of the
+// wave needs it.  Callers must not use the result for denormal a (the
+// triangle test rejects |a| < 1e-4 before f matters).
+__device__ __forceinline__ float recip_normal(float a) {
+  float f = recip_newton(a);
+  if (__builtin_expect(!(__builtin_fabsf(a) < 0x1p126f), 0)) f = 1.0f / a;
+  return f;
+}
+
+// IntersectsTriangle (ray_intersects.glsl:61-96, Moller-Trumbore with edges
+// precomputed at upload) evaluated without branches: every quantity the reference
+// computes on its way to each early return is computed, and the accept
+// predicate is their conjunction -- the same decision and the same t
+// (f = 1 / a is the correctly rounded division of the reference).
+__device__ __forceinline__ bool tri_accept(f3 o, f3 d, float4 A, float4 B, float4 C, float dist, float& tout) {
+  const f3 v0 = mk(A.x, A.y, A.z), e1 = mk(A.w, B.x, B.y), e2 = mk(B.z, B.w, C.x);
+  const f3 h = cross(d, e2);
+  const float a = dot(e1, h);
+  const bool parallel = (a > -0.0001f) & (a < 0.0001f);
+  const float f = recip_normal(a);  // |a| < 1e-4 is rejected (parallel)
+  const f3 s = o - v0;
+  const float u = f * dot(s, h);
+  const f3 q = cross(s, e1);
+  const float v = f * dot(d, q);
+  const float t = f * dot(e2, q);
+  tout = t;
+  return !parallel & !((u < 0.0f) | (u > 1.0f)) & !((v < 0.0f) | (u + v > 1.0f)) & (t > 0.00001f) & (t < dist);
+}
+
+// tri_accept split in two for the leaf step: the part up to the reciprocal
+// (true when |a| needs the division: recip_normal's fallback range), then the rest.
+struct TriPrep {
+  f3 v0, e1, e2, h;
+  float a, f;
+};
+__device__ __forceinline__ bool tri_prep(f3 d, float4 A, float4 B, float4 C, TriPrep& p) {
+  p.v0 = mk(A.x, A.y, A.z);
+  p.e1 = mk(A.w, B.x, B.y);
+  p.e2 = mk(B.z, B.w, C.x);
+  p.h = cross(d, p.e2);
+  p.a = dot(p.e1, p.h);
+  p.f = recip_newton(p.a);
+  return !(__builtin_fabsf(p.a) < 0x1p126f);
+}
+__device__ __forceinline__ bool tri_finish(f3 o, f3 d, const TriPrep& p, float dist, float& tout) {
+  const bool parallel = (p.a > -0.0001f) & (p.a < 0.0001f);
+  const f3 s = o - p.v0;
+  const float u = p.f * dot(s, p.h);
+  const f3 q = cross(s, p.e1);
+  const float v = p.f * dot(d, q);
+  const float t = p.f * dot(p.e2, q);
+  tout = t;
+  return !parallel & !((u < 0.0f) | (u > 1.0f)) & !((v < 0.0f) | (u + v > 1.0f)) & (t > 0.00001f) & (t < dist);
+}
+
+// Depth-first traversal in the reference's pop order (right child first).
+// Each child's box is tested once, when its parent is expanded; a child that
+// fails is never pushed (the running distance only shrinks, so it would fail
+// at its pop too); a pushed child is re-checked against the distance at pop
+// time with its stored entry distance (the same value IntersectsBox returns).
+// `any`: stop at the first accepted triangle (shadow rays, CheckHit(...).hit).
+template <bool COUNT, bool LDSM>
+__device__ uint32_t traverse(const KParams& kp, const Lane& ln, Counters& c, uint32_t root, f3 o, f3 d,
+                             float& dist, bool any) {
+  // Flat loop: each iteration performs ONE step for the lane -- test one
+  // triangle of the current leaf, expand the current internal node, or pop --
+  // so lanes at leaves and lanes at internal nodes advance together.
+  // `ref`/`cnt` describe the current node as the reference's node record does
+  // (leaf: first triangle + remaining count; internal: index of its first
+  // child, cnt == 0); kNone = nothing current, pop next.
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  const f3 inv = mk(recip_exact(d.x), recip_exact(d.y), recip_exact(d.z));
+  uint32_t hit = kNone;
+  const float4 rlo = node4<LDSM>(kp, 2 * root + 2), rhi = node4<LDSM>(kp, 2 * root + 3);
+  bump<COUNT>(c, ST_NODES);
+  if (!box_ok(box_t(o, inv, rlo, rhi), dist)) return hit;
+  uint32_t ref = __float_as_uint(rlo.w), cnt = __float_as_uint(rhi.w);
+  int sp = 0;
+  for (;;) {
+    if (cnt > 0) {
+      // leaf: one triangle per step, in the reference's order
+      bump<COUNT>(c, ST_TRIS);
+      const uint32_t t3 = 3 * ref;
+      float tt;
+      if (tri_accept(o, d, tri4<LDSM>(kp, t3), tri4<LDSM>(kp, t3 + 1), tri4<LDSM>(kp, t3 + 2), dist, tt)) {
+        dist = tt;
+        hit = ref;
+        if (any) break;
+      }
+      ++ref;
+      if (--cnt == 0) ref = kNone;
+    } else if (ref != kNone) {
+      // internal: test both children now.  The reference pushes c0 then c1
+      // and pops c1 first; a child whose box fails is never needed (the
+      // distance only shrinks), a lone passing child is visited directly.
+      const uint32_t pi = 2 * ref + 2;
+      const float4 l0 = node4<LDSM>(kp, pi), h0 = node4<LDSM>(kp, pi + 1);
+      const float4 l1 = node4<LDSM>(kp, pi + 2), h1 = node4<LDSM>(kp, pi + 3);
+      bump<COUNT>(c, ST_NODES, 2);
+      const float b0 = box_t(o, inv, l0, h0);
+      const float b1 = box_t(o, inv, l1, h1);
+      const bool v0 = box_ok(b0, dist), v1 = box_ok(b1, dist);
+      const uint32_t r0 = __float_as_uint(l0.w), n0 = __float_as_uint(h0.w);
+      if (v0 & v1) {
+        if (sp >= kp.stack_entries) {  // cannot happen for a validated BVH
+          bump<COUNT>(c, ST_OVERFLOW);
+          break;
+        }
+        stk_push<LDSM>(ln, sp, r0, n0, b0);
+        ++sp;
+        if constexpr (COUNT) {
+          if ((uint32_t)sp > c.v[ST_MAXSTACK]) c.v[ST_MAXSTACK] = (uint32_t)sp;
+        }
+      }
+      ref = v1 ? __float_as_uint(l1.w) : (v0 ? r0 : kNone);
+      cnt = v1 ? __float_as_uint(h1.w) : (v0 ? n0 : 0u);
+    }
+    if (cnt == 0 && ref == kNone) {
+      // pop one entry; it is visited if it still beats the running distance
+      if (sp == 0) break;
+      --sp;
+      if (stk_t<LDSM>(ln, sp) < dist) stk_ref<LDSM>(ln, sp, ref, cnt);
+    }
+  }
+  return hit;
+}
+
+__device__ __forceinline__ f3 xform(const float* m, f3 v, float w) {
+  return mk(((m[0] * v.x + m[4] * v.y) + m[8] * v.z) + m[12] * w,
+            ((m[1] * v.x + m[5] * v.y) + m[9] * v.z) + m[13] * w,
+            ((m[2] * v.x + m[6] * v.y) + m[10] * v.z) + m[14] * w);
+}
+
+// CheckHit over the model BVHs (raytrace_compute.glsl:143-162): closest hit
+// triangle (dist updated), or with `any` the first accepted triangle.
+template <bool COUNT, bool LDSM>
+__device__ uint32_t trace_mesh(const KParams& kp, const Lane& ln, Counters& c, f3 ro, f3 rd, float& dist, bool any) {
+  uint32_t hit_tri = 0xFFFFFFFFu;
+  for (uint32_t i = 0; i < kp.bvh_count; ++i) {
+    const srt_bvh_record& b = kp.bvhs[i];
+    const f3 to = xform(b.frame, ro, 1.0f);
+    const f3 td = xform(b.frame, rd, 0.0f);
+    const uint32_t h = traverse<COUNT, LDSM>(kp, ln, c, b.first_index, to, td, dist, any);
+    if (h != 0xFFFFFFFFu) {
+      hit_tri = h;
+      if (any) break;
+    }
+  }
+  return hit_tri;
+}
+
+struct Trav {
+  f3 o, d, inv;       // ray in the current BVH's frame
+  float dist;         // running intersection_distance
+  uint32_t ref, cnt;  // current node (leaf: first triangle + remaining; internal: first child)
+  uint32_t hit;       // best triangle so far (0xFFFFFFFF: none)
+  uint32_t bi;        // current BVH
+  int sp;
+  int lo;             // global-scene mode: entries [lo, sp) are in the LDS ring, [0, lo) in HBM
+  bool active;        // still traversing
+  bool start;         // next step sets up BVH `bi`
+};
+
+constexpr uint32_t kNoneRef = 0xFFFFFFFFu;
+#ifndef SRT_LEAF_TRIS
+#define SRT_LEAF_TRIS 2
+#endif
+constexpr int kLeafTris = SRT_LEAF_TRIS;  // triangles tested per leaf step
+// Sub-steps of one traversal iteration: 'I' expands an internal node, 'L'
+// tests a leaf's next triangles; each is followed by a pop if nothing is current.
+#ifndef SRT_STEP_PATTERN
+#define SRT_STEP_PATTERN "ILILILIL"
+#endif
+constexpr char kStepPattern[] = SRT_STEP_PATTERN;
+// global-scene mode: entries per lane kept in the LDS ring (power of two)
+#ifndef SRT_SHORT_STACK
+#define SRT_SHORT_STACK 16
+#endif
+constexpr int kShortStack = SRT_SHORT_STACK;
+// consecutive 64-item batches a wave claims per atomic on the launch's batch counter
+#ifndef SRT_CLAIM
+#define SRT_CLAIM 4
+#endif
+constexpr int kClaim = SRT_CLAIM;
+static_assert((kShortStack & (kShortStack - 1)) == 0, "kShortStack must be a power of two");
+constexpr int kTriPad = 3;                // zero records past the triangle array (>= kLeafTris - 1)
+static_assert(kLeafTris >= 1 && kLeafTris - 1 <= kTriPad, "kLeafTris");
+
+// Sets up BVH `t.bi` for the world ray (the reference's per-model transform,
+// raytrace_compute.glsl:146-147) and tests its root box.
+template <bool COUNT, bool LDSM>
+__device__ __forceinline__ void trav_begin_bvh(const KParams& kp, Counters& c, Trav& t, f3 ro, f3 rd) {
+  const srt_bvh_record& b = kp.bvhs[t.bi];
+  t.o = xform(b.frame, ro, 1.0f);
+  t.d = xform(b.frame, rd, 0.0f);
+  t.inv = mk(recip_exact(t.d.x), recip_exact(t.d.y), recip_exact(t.d.z));
+  const uint32_t root = b.first_index;
+  const float4 rlo = node4<LDSM>(kp, 2 * root + 2), rhi = node4<LDSM>(kp, 2 * root + 3);
+  bump<COUNT>(c, ST_NODES);
+  const bool ok = box_ok(box_t(t.o, t.inv, rlo, rhi), t.dist);
+  t.ref = ok ? __float_as_uint(rlo.w) : kNoneRef;
+  t.cnt = ok ? __float_as_uint(rhi.w) : 0u;
+  t.sp = 0;
+  t.lo = 0;
+  t.start = false;
+}
+
+// Leaf sub-step: up to kLeafTris triangles of the current leaf, in order: each
+// is tested against the distance the previous one left; a shadow ray stops at
+// its first accept (the triangle array is padded with kTriPad zero records).
+template <bool COUNT, bool LDSM>
+__device__ __forceinline__ void trav_leaf(const KParams& kp, Counters& c, Trav& t, bool any) {
+  const uint32_t n = t.cnt < (uint32_t)kLeafTris ? t.cnt : (uint32_t)kLeafTris;
+  bump<COUNT>(c, ST_TRIS, n);
+  float dist = t.dist;
+  uint32_t hit = t.hit;
+  bool stop = false;
+  const float4* tp = tri_ptr<LDSM>(kp, t.ref);
+  // all triangles' loads and reciprocals first (one shared fallback branch),
+  // so the triangles' arithmetic overlaps; then the tests in order
+  TriPrep pr[kLeafTris];
+  bool slow = false;
+#pragma unroll
+  for (int k = 0; k < kLeafTris; ++k) slow |= tri_prep(t.d, tp[3 * k], tp[3 * k + 1], tp[3 * k + 2], pr[k]);
+  if (__builtin_expect(slow, 0)) {
+#pragma unroll
+    for (int k = 0; k < kLeafTris; ++k) pr[k].f = 1.0f / pr[k].a;
+  }
+#pragma unroll
+  for (int k = 0; k < kLeafTris; ++k) {
+    float tk;
+    const bool tk_ok = tri_finish(t.o, t.d, pr[k], dist, tk);
+    const bool ak = k == 0 ? tk_ok : (((uint32_t)k < n) & !stop & tk_ok);  // a leaf holds >= 1 triangle
+    dist = ak ? tk : dist;
+    hit = ak ? t.ref + k : hit;
+    stop = stop | (ak & any);
+  }
+  t.dist = dist;
+  t.hit = hit;
+  t.ref += n;
+  t.cnt -= n;
+  t.active = !stop;
+  t.ref = (t.cnt == 0 || stop) ? kNoneRef : t.ref;
+  t.cnt = stop ? 0u : t.cnt;
+}
+
+// Internal sub-step: test both children's boxes; push c0 when both pass, go to
+// c1 if it passes, else to c0 if it passes.
+template <bool COUNT, bool LDSM, bool PACK>
+__device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln, Counters& c, Trav& t) {
+  const uint32_t pi = 2 * t.ref + 2;
+  const float4 l0 = node4<LDSM>(kp, pi), h0 = node4<LDSM>(kp, pi + 1);
+  const float4 l1 = node4<LDSM>(kp, pi + 2), h1 = node4<LDSM>(kp, pi + 3);
+  bump<COUNT>(c, ST_NODES, 2);
+  const float b0 = box_t(t.o, t.inv, l0, h0);
+  const float b1 = box_t(t.o, t.inv, l1, h1);
+  const bool v0 = box_ok(b0, t.dist), v1 = box_ok(b1, t.dist);
+  const uint32_t r0 = __float_as_uint(l0.w), n0 = __float_as_uint(h0.w);
+  // the c0 slot is written unconditionally (it is free either way; the stack
+  // holds depth + 1 entries, validated at upload)
+  if constexpr (LDSM) {
+    slot_write<true>(ln.stk, ln.stride, t.sp, r0, n0, b0);
+  } else {
+    if (t.sp - t.lo == kShortStack) {  // ring full: its oldest entry moves to HBM (rare)
+      uint32_t r, n;
+      float bt;
+      slot_read<PACK>(ln.stk, ln.stride, t.lo & (kShortStack - 1), r, n, bt);
+      slot_write<PACK>(ln.gstk, ln.gstride, t.lo, r, n, bt);
+      ++t.lo;
+    }
+    slot_write<PACK>(ln.stk, ln.stride, t.sp & (kShortStack - 1), r0, n0, b0);
+  }
+  t.sp += (v0 & v1) ? 1 : 0;
+  if constexpr (COUNT) {
+    if ((uint32_t)t.sp > c.v[ST_MAXSTACK]) c.v[ST_MAXSTACK] = (uint32_t)t.sp;
+  }
+  t.ref = v1 ? __float_as_uint(l1.w) : (v0 ? r0 : kNoneRef);
+  t.cnt = v1 ? __float_as_uint(h1.w) : (v0 ? n0 : 0u);
+}
+
+// Nothing current: pop one entry (visited if it still beats the running
+// distance), or finish this BVH.  A lane whose next BVH is pending (`start`,
+// set up at the next iteration) does nothing.
+template <bool LDSM, bool PACK>
+__device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav& t, bool any) {
+  if (t.active & !t.start & (t.cnt == 0) & (t.ref == kNoneRef)) {
+    if (t.sp > 0) {
+      --t.sp;
+      uint32_t r, n;
+      float et;
+      if constexpr (LDSM) {
+        slot_read<true>(ln.stk, ln.stride, t.sp, r, n, et);
+      } else if (t.sp < t.lo) {  // below the LDS ring: from HBM (rare)
+        slot_read<PACK>(ln.gstk, ln.gstride, t.sp, r, n, et);
+        t.lo = t.sp;
+      } else {
+        slot_read<PACK>(ln.stk, ln.stride, t.sp & (kShortStack - 1), r, n, et);
+      }
+      const bool take = et < t.dist;
+      t.ref = take ? r : kNoneRef;
+      t.cnt = take ? n : 0u;
+    } else if ((any && t.hit != kNoneRef) || t.bi + 1 >= kp.bvh_count) {
+      t.active = false;  // CheckHit's loop over bvh_count is complete
+    } else {
+      ++t.bi;
+      t.start = true;
+    }
+  }
+}
+
+template <bool COUNT, bool LDSM, bool PACK, int K>
+__device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln, Counters& c, Trav& t, bool any) {
+  if constexpr (kStepPattern[K] != 0) {
+    if constexpr (kStepPattern[K] == 'I') {
+      DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K, t.cnt == 0 && t.ref != kNoneRef);
+      if (t.cnt == 0 && t.ref != kNoneRef) trav_internal<COUNT, LDSM, PACK>(kp, ln, c, t);
+    } else {
+      DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K, t.cnt > 0);
+      if (t.cnt > 0) trav_leaf<COUNT, LDSM>(kp, c, t, any);
+    }
+    DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K + 2, t.active & !t.start & (t.cnt == 0) & (t.ref == kNoneRef));
+    trav_pop<LDSM, PACK>(kp, ln, t, any);
+    trav_substeps<COUNT, LDSM, PACK, K + 1>(kp, ln, c, t, any);
+  }
+}
+
+// One traversal iteration (see traverse() for the order argument): the
+// sub-steps of kStepPattern in turn, each taken by the lanes whose current
+// node is of its kind, so a lane makes up to strlen(kStepPattern) steps of
+// its own sequence per iteration, in order.  `any` selects the shadow-ray
+// (first hit) variant.
+template <bool COUNT, bool LDSM, bool PACK>
+__device__ __forceinline__ void trav_step(const KParams& kp, const Lane& ln, Counters& c, Trav& t, f3 ro, f3 rd,
+                                          bool any) {
+  if (t.start) trav_begin_bvh<COUNT, LDSM>(kp, c, t, ro, rd);  // only for BVHs after the first
+  trav_substeps<COUNT, LDSM, PACK, 0>(kp, ln, c, t, any);
+}
+
+}  // namespace srt

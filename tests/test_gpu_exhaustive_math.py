@@ -1,6 +1,6 @@
 """Exhaustive checks (all 2^32 fp32 inputs, on the GPU) of the kernel's fast exact arithmetic.
 
-* recip_normal (pathtrace.hip): the triangle test's f = 1.0 / a (ray_intersects.glsl:61-96)
+* recip_normal (csrc/traversal.hpp): the triangle test's f = 1.0 / a (ray_intersects.glsl:61-96)
   as v_rcp_f32 + one FMA Newton step for 2^-126 <= |a| < 2^126, the division elsewhere.
   Every mismatch against the correctly rounded quotient must lie outside that range
   (exponent field 0, 253, 254 or 255).
