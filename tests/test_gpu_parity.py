@@ -253,3 +253,21 @@ def test_save_image_matches_output(rubik, tmp_path):
     finally:
         r.close()
     assert (_read_png(tmp_path / "frame.png") == out[::-1]).all()
+
+
+@pytest.mark.parametrize("yaw,pitch,origin", [(25.0, -12.0, (3.0, 12.0, 30.0)), (-70.0, 40.0, (-14.0, 6.0, 14.0)),
+                                              (180.0, -89.0, (0.5, 25.0, 0.25))])
+def test_moved_camera_parity(rubik, yaw, pitch, origin):
+    """Camera::Rotate / a moved origin (the reference's interactive path, camera.cpp:107-212): rays leave the
+    cube at grazing and inside-out angles, through the box faces the default camera never sees."""
+    setup = R.make_setup(48, 40, show_model=True, models=[rubik])
+    setup.camera.Rotate(yaw, pitch)
+    setup.camera.position = np.asarray(origin, np.float32)
+    assert_parity(setup, 2)
+
+
+def test_moved_camera_spheres_parity():
+    setup = R.make_setup(40, 48, show_model=False)
+    setup.camera.Rotate(-35.0, 20.0)
+    setup.camera.position = np.asarray((1.5, 0.5, 2.0), np.float32)
+    assert_parity(setup, 3)
