@@ -168,10 +168,15 @@ class Model {
   srt_model* m_;
 };
 
-// model_loader.cpp:20-32: objects/<name>/<name>.obj
-inline std::unique_ptr<Model> LoadObject(const std::string& name, const std::string& objects_dir = "./objects/") {
+// model_loader.cpp:20-32: objects/<name>/<name>.obj.  texcoords = true is the
+// loader with has_texcoords set (vertex uvs from `vt`; the reference leaves
+// them at (0,0)), and its textures are then sampled per hit.
+inline std::unique_ptr<Model> LoadObject(const std::string& name, const std::string& objects_dir = "./objects/",
+                                         bool texcoords = false) {
   srt_model* m = nullptr;
-  check(srt_model_load((objects_dir + name + "/" + name + ".obj").c_str(), &m), "LoadObject");
+  check(srt_model_load_ex((objects_dir + name + "/" + name + ".obj").c_str(), texcoords ? SRT_LOAD_TEXCOORDS : 0u,
+                          &m),
+        "LoadObject");
   return std::make_unique<Model>(m);
 }
 

@@ -43,6 +43,9 @@ typedef struct { float diffuse[3]; float specular_ex; float specular[3]; uint32_
 typedef struct { uint32_t v0_idx, v1_idx, v2_idx, material_idx; } srt_triangle;                 /* 16 B */
 typedef struct { float vertex[3]; float pad0; float texture[2]; float pad1[2]; } srt_vertex;    /* 32 B */
 typedef struct { float position[3]; float intensity; float color[3]; float pad1; } srt_light;  /* 32 B, raytracer/light.h:54-63 */
+/* A decoded 8-bit texture as stb_image returns it (gpu_texture.h:29-33): rows
+ * top first, `channels` (1-4) interleaved bytes per texel. */
+typedef struct { const uint8_t* texels; int32_t width, height, channels; } srt_texture;
 typedef struct { float origin[3]; float pad0; float direction[3]; float intersection_distance; } srt_ray; /* 32 B, common/types.h:15-35 */
 
 /* Work counters of a counting launch. */
@@ -113,14 +116,28 @@ int srt_local_rows(srt_context* ctx);
 /* ===================== bindings (SSBOs / texel buffers / images) ===================== */
 /* AssetUtils::UploadModelDataToGPU (include/asset_utils/gpu_loader.h:19,
  * src/asset_utils/gpu_loader.cpp:63-183): the five SSBOs at bindings 5..9.
- * tex_albedo: 3 floats per material = the texture() result for use_texture
- * materials (may be NULL when none use textures). */
+ * Materials with use_texture take their albedo from `tex_albedo` (3 floats
+ * per material: the texture() result, constant because the reference's
+ * loader leaves every uv at (0,0), types.h:105) when it is non-NULL.  When it
+ * is NULL they sample texture `handle` (64-bit, handle[0] | handle[1] << 32;
+ * see srt_upload_textures) at the hit's interpolated uv, as
+ * TriangleToSupportedMat does (raytrace_utils.glsl:144-166); an unknown
+ * handle samples as zero.  Sampling needs the BVH records that can hit
+ * (non-zero frame) to own disjoint triangle ranges, as UploadModelDataToGPU
+ * builds them (checked at dispatch). */
 int srt_upload_scene(srt_context* ctx,
                      const srt_bvh_record* bvhs, uint32_t n_bvhs,
                      const srt_bvh_node* nodes, uint32_t n_nodes,
                      const srt_material_obj* mats, const float* tex_albedo, uint32_t n_mats,
                      const srt_triangle* tris, uint32_t n_tris,
                      const srt_vertex* verts, uint32_t n_verts);
+/* GPUTexture(file, true) + GetHandle() (gpu_texture.h:24-68,133-137): the
+ * textures sampled by use_texture materials; texture i gets handle i.
+ * Replaces any previous set.  Sampling contract:
+ * level 0, GL_LINEAR, GL_REPEAT, texels c/255. */
+int srt_upload_textures(srt_context* ctx, const srt_texture* textures, uint32_t n);
+/* The same sampler on the host: texture(sampler2D, vec2(s, t)).xyz. */
+int srt_texture_sample(const srt_texture* tex, float s, float t, float rgb[3]);
 /* AssetUtils::UpdateModelMatrix (gpu_loader.cpp:185-196). */
 int srt_update_model_matrix(srt_context* ctx, uint32_t index, const float frame[16]);
 /* light SSBO at binding 4 (src/main.cpp:688-692). */
@@ -165,6 +182,11 @@ int srt_trace_closest(srt_context* ctx, const srt_ray* rays, uint32_t n, uint32_
  * (include/intersection_utils/bvh.h:40-148).  `obj_path` is the .obj file;
  * MTL files resolve relative to its directory. */
 int srt_model_load(const char* obj_path, srt_model** out);
+/* srt_model_load with flags.  SRT_LOAD_TEXCOORDS gives each vertex the uv of
+ * its face's `vt` index, i.e. the loader with has_texcoords set
+ * (model_loader.cpp:322-324), which the reference never does. */
+#define SRT_LOAD_TEXCOORDS 1u
+int srt_model_load_ex(const char* obj_path, uint32_t flags, srt_model** out);
 /* Build a model from raw triangles (one material). */
 int srt_model_from_triangles(const float* xyz9, uint32_t n_tris, const float kd[3], const float ks[3], float ns,
                              srt_model** out);
@@ -179,6 +201,13 @@ int srt_scene_free(srt_scene* s);
 int srt_scene_sizes(const srt_scene* s, uint32_t sizes[5]);
 int srt_scene_copy(const srt_scene* s, srt_bvh_record* bvhs, srt_bvh_node* nodes, srt_material_obj* mats,
                    float* tex_albedo, srt_triangle* tris, srt_vertex* verts);
+/* Textures of the scene's use_texture materials (material handle = index);
+ * sample_textures = 1 when a model was loaded with SRT_LOAD_TEXCOORDS. */
+int srt_scene_texture_count(const srt_scene* s, uint32_t* n, int* sample_textures);
+/* Texture i; `out->texels` points into the scene (valid while it lives). */
+int srt_scene_texture(const srt_scene* s, uint32_t i, srt_texture* out);
+/* srt_upload_scene of the flattened arrays; with sample_textures it also
+ * uploads the textures and passes tex_albedo = NULL. */
 int srt_upload_scene_obj(srt_context* ctx, const srt_scene* s);
 
 /* Noise texel buffers of UpdateNoiseTex (src/main.cpp:269-301) from the

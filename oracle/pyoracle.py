@@ -22,7 +22,8 @@ P = C.c_void_p
 class OrScene(C.Structure):
     _fields_ = [("bvhs", P), ("n_bvhs", C.c_uint32), ("nodes", P), ("n_nodes", C.c_uint32), ("mats", P),
                 ("n_mats", C.c_uint32), ("tex_albedo", P), ("tris", P), ("n_tris", C.c_uint32), ("verts", P),
-                ("n_verts", C.c_uint32), ("lights", P), ("n_lights", C.c_uint32), ("noise", P), ("noise_u", P)]
+                ("n_verts", C.c_uint32), ("lights", P), ("n_lights", C.c_uint32), ("noise", P), ("noise_u", P),
+                ("tex_texels", P), ("tex_info", P), ("n_tex", C.c_uint32)]
 
 
 class OrFrame(C.Structure):
@@ -91,9 +92,21 @@ class Oracle:
             s.bvhs, s.n_bvhs = _p(bvhs), len(bvhs)
             s.nodes, s.n_nodes = _p(nodes), len(nodes)
             s.mats, s.n_mats = _p(mats), len(mats)
-            s.tex_albedo = _p(np.ascontiguousarray(tex, np.float32))
             s.tris, s.n_tris = _p(tris), len(tris)
             s.verts, s.n_verts = _p(verts), len(verts)
+            if getattr(scene, "sample_textures", False):
+                # TriangleToSupportedMat samples texture `handle` at the hit's uv
+                texs = [t if t.ndim == 3 else t[:, :, None] for t in scene.textures]
+                info = np.zeros((max(len(texs), 1), 4), np.uint32)
+                first = 0
+                for i, t in enumerate(texs):
+                    info[i] = (first, t.shape[1], t.shape[0], t.shape[2])
+                    first += t.shape[0] * t.shape[1] * t.shape[2]
+                texels = np.concatenate([t.reshape(-1) for t in texs] or [np.zeros(1, np.uint8)]).astype(np.uint8)
+                self._keep += [info, texels]
+                s.tex_texels, s.tex_info, s.n_tex = _p(texels), _p(info), len(texs)
+            else:
+                s.tex_albedo = _p(np.ascontiguousarray(tex, np.float32))
         if lights is not None:
             la = np.ascontiguousarray(lights)
             self._keep.append(la)

@@ -335,16 +335,83 @@ static uint32_t intersects(const OrScene* s, uint32_t start, v3 o, v3 d, float* 
   return out;
 }
 
-/* raytrace_utils.glsl:140-175 TriangleToSupportedMat (uv == (0,0): types.h:105) */
-static Material tri_material(const OrScene* s, uint32_t tri_idx, OrStats* st) {
+/* One 8-bit texel channel as GL reads it: c/255; GL_RED has no g/b, and the
+ * reference uploads a 2-channel file as GL_RGB (read here as (r, g, 0)). */
+static float texel_channel(const uint8_t* px, uint32_t ch, uint32_t k) {
+  if (k >= ch || (ch == 2 && k == 2)) return 0.0f;
+  return (float)px[k] / 255.0f;
+}
+
+/* texture(sampler2D, st).xyz for the reference's sampler state
+ * (gpu_texture.h:52-58: GL_REPEAT, GL_LINEAR magnification; a compute shader
+ * samples level 0).  Contract: non-finite coordinates
+ * read as 0; wrap by st - floor(st); bilinear over texel centres
+ * (i + 0.5)/size with weights (1-a)(1-b), a(1-b), (1-a)b, ab summed in that
+ * order. */
+static v3 texture_bilinear(const OrScene* s, uint32_t h, float sc, float tc) {
+  const uint32_t* in = s->tex_info + 4 * (size_t)h;
+  const int w = (int)in[1], hh = (int)in[2];
+  const uint32_t ch = in[3];
+  if (!isfinite(sc)) sc = 0.0f;
+  if (!isfinite(tc)) tc = 0.0f;
+  sc -= floorf(sc);
+  tc -= floorf(tc);
+  float x = sc * (float)w - 0.5f, y = tc * (float)hh - 0.5f;
+  float xf = floorf(x), yf = floorf(y);
+  float a = x - xf, b = y - yf;
+  int xi[2] = {(int)xf, (int)xf + 1}, yi[2] = {(int)yf, (int)yf + 1};
+  if (xi[0] < 0) xi[0] = w - 1;
+  if (yi[0] < 0) yi[0] = hh - 1;
+  if (xi[1] >= w) xi[1] = 0;
+  if (yi[1] >= hh) yi[1] = 0;
+  const float wt[4] = {(1.0f - a) * (1.0f - b), a * (1.0f - b), (1.0f - a) * b, a * b};
+  float out[3];
+  for (uint32_t k = 0; k < 3; k++) {
+    float acc = 0.0f;
+    for (int q = 0; q < 4; q++) {
+      const uint8_t* px = s->tex_texels + in[0] + ((size_t)yi[q >> 1] * (size_t)w + (size_t)xi[q & 1]) * ch;
+      const float term = wt[q] * texel_channel(px, ch, k);
+      acc = q == 0 ? term : acc + term;
+    }
+    out[k] = acc;
+  }
+  return V(out[0], out[1], out[2]);
+}
+
+static OrVertex vertex_at(const OrScene* s, uint32_t i) {
+  if (i < s->n_verts) return s->verts[i];
+  OrVertex z; memset(&z, 0, sizeof z); return z;
+}
+
+/* raytrace_utils.glsl:140-175 TriangleToSupportedMat; model_p is the hit in
+ * the hit BVH's frame (raytrace_compute.glsl:155) */
+static Material tri_material(const OrScene* s, uint32_t tri_idx, v3 model_p, OrStats* st) {
   Material m;
   OrTri tri;
   if (tri_idx < s->n_tris) tri = s->tris[tri_idx]; else memset(&tri, 0, sizeof tri);
   OrMaterial in;
   if (tri.mat < s->n_mats) in = s->mats[tri.mat]; else memset(&in, 0, sizeof in);
   st->mat_reads++;
-  if (in.use_texture == 0) m.albedo = vload(in.diffuse);
-  else m.albedo = s->tex_albedo ? vload(s->tex_albedo + (size_t)tri.mat * 3) : V(0, 0, 0);
+  if (in.use_texture == 0) {
+    m.albedo = vload(in.diffuse);
+  } else if (s->tex_albedo) {  /* every uv is (0,0) (types.h:105): the constant texture() result */
+    m.albedo = vload(s->tex_albedo + (size_t)tri.mat * 3);
+  } else {  /* :145-166 */
+    OrVertex t0 = vertex_at(s, tri.v[0]), t1 = vertex_at(s, tri.v[1]), t2 = vertex_at(s, tri.v[2]);
+    v3 v0v1 = sub(vload(t1.pos), vload(t0.pos));
+    v3 v0v2 = sub(vload(t2.pos), vload(t0.pos));
+    v3 v0p = sub(model_p, vload(t0.pos));
+    float d00 = dot(v0v1, v0v1), d01 = dot(v0v1, v0v2), d11 = dot(v0v2, v0v2);
+    float d20 = dot(v0p, v0v1), d21 = dot(v0p, v0v2);
+    float denom = 1.0f / (d00 * d11 - d01 * d01);
+    float v = (d11 * d20 - d01 * d21) * denom;
+    float w = (d00 * d21 - d01 * d20) * denom;
+    float u = 1.0f - v - w;
+    float sc = u * t0.uv[0] + v * t1.uv[0] + w * t2.uv[0];
+    float tc = u * t0.uv[1] + v * t1.uv[1] + w * t2.uv[1];
+    uint64_t h = (uint64_t)in.handle[0] | ((uint64_t)in.handle[1] << 32);
+    m.albedo = h < s->n_tex ? texture_bilinear(s, (uint32_t)h, sc, tc) : V(0, 0, 0);
+  }
   m.specular = vload(in.Ks);
   m.roughness = 1.0f / (in.Ns + 0.0000001f);
   m.metalness = 0.1f;
@@ -418,7 +485,8 @@ static HitRecord check_hit(Ctx* c, v3 ro, v3 rd, float mn, float mx) {
         rec.p = add(smul(dist, rd), ro);
         rec.normal = tri_norm;
         rec.t = dist;
-        rec.mat = tri_material(c->s, hit, c->st);
+        v3 model_p = add(smul(dist, td), to);
+        rec.mat = tri_material(c->s, hit, model_p, c->st);
       }
     }
   }

@@ -48,12 +48,19 @@ typedef struct {
   const OrBVH* bvhs;       uint32_t n_bvhs;      /* real records; bvhs[i>=n] read as zeros */
   const OrNode* nodes;     uint32_t n_nodes;
   const OrMaterial* mats;  uint32_t n_mats;
-  const float* tex_albedo; /* 3 floats per material: texture(sampler, uv) result, used when use_texture */
+  const float* tex_albedo; /* 3 floats per material: texture(sampler, uv) result, used when use_texture
+                              (NULL: sample tex_* at the hit's uv) */
   const OrTri* tris;       uint32_t n_tris;
   const OrVertex* verts;   uint32_t n_verts;
   const OrLight* lights;   uint32_t n_lights;  /* lights[i >= n_lights] reads as zeros */
   const float* noise;      /* RGB32F, W*H texels (binding 1, noiseTex) */
   const float* noise_u;    /* RGB32F, W*H texels (binding 2, noiseUniformTex) */
+  /* textures sampled by use_texture materials when tex_albedo is NULL:
+   * texture h = material handle, tex_info[4h..4h+3] = first byte, width,
+   * height, channels; tex_texels = 8-bit texels (stb_image layout) */
+  const uint8_t* tex_texels;
+  const uint32_t* tex_info;
+  uint32_t n_tex;
 } OrScene;
 
 /* The per-dispatch uniforms (raytrace_compute.glsl:18-31,39; ray_intersects.glsl:8) */

@@ -14,10 +14,12 @@ struct srt_scene {
 
 extern "C" {
 
-int srt_model_load(const char* obj_path, srt_model** out) {
-  if (!obj_path || !out) return SRT_ERR_INVALID;
+int srt_model_load(const char* obj_path, srt_model** out) { return srt_model_load_ex(obj_path, 0, out); }
+
+int srt_model_load_ex(const char* obj_path, uint32_t flags, srt_model** out) {
+  if (!obj_path || !out || (flags & ~SRT_LOAD_TEXCOORDS)) return SRT_ERR_INVALID;
   std::string err;
-  auto m = srt::LoadObjectFile(obj_path, &err);
+  auto m = srt::LoadObjectFile(obj_path, (flags & SRT_LOAD_TEXCOORDS) != 0, &err);
   if (!m) {
     srt::SetError(err);
     return SRT_ERR_IO;
@@ -103,12 +105,40 @@ int srt_scene_copy(const srt_scene* s, srt_bvh_record* bvhs, srt_bvh_node* nodes
   return SRT_OK;
 }
 
+int srt_scene_texture_count(const srt_scene* s, uint32_t* n, int* sample_textures) {
+  if (!s) return SRT_ERR_INVALID;
+  if (n) *n = (uint32_t)s->s->textures.size();
+  if (sample_textures) *sample_textures = s->s->sample_textures ? 1 : 0;
+  return SRT_OK;
+}
+
+int srt_scene_texture(const srt_scene* s, uint32_t i, srt_texture* out) {
+  if (!s || !out || i >= s->s->textures.size()) return SRT_ERR_INVALID;
+  const srt::Texture& t = s->s->textures[i];
+  *out = srt_texture{t.texels.data(), t.width, t.height, t.channels};
+  return SRT_OK;
+}
+
+int srt_texture_sample(const srt_texture* tex, float s, float t, float rgb[3]) {
+  if (!tex || !tex->texels || !rgb || tex->width <= 0 || tex->height <= 0 || tex->channels < 1 || tex->channels > 4)
+    return SRT_ERR_INVALID;
+  srt::TextureSample(tex->texels, tex->width, tex->height, tex->channels, s, t, rgb);
+  return SRT_OK;
+}
+
 int srt_upload_scene_obj(srt_context* ctx, const srt_scene* s) {
   if (!ctx || !s) return SRT_ERR_INVALID;
   const srt::Scene& sc = *s->s;
+  if (sc.sample_textures) {
+    std::vector<srt_texture> tx;
+    for (const auto& t : sc.textures) tx.push_back(srt_texture{t.texels.data(), t.width, t.height, t.channels});
+    const int rc = srt_upload_textures(ctx, tx.data(), (uint32_t)tx.size());
+    if (rc) return rc;
+  }
   return srt_upload_scene(ctx, sc.bvhs.data(), (uint32_t)sc.bvhs.size(), sc.nodes.data(), (uint32_t)sc.nodes.size(),
-                          sc.mats.data(), sc.tex_albedo.data(), (uint32_t)sc.mats.size(), sc.tris.data(),
-                          (uint32_t)sc.tris.size(), sc.verts.data(), (uint32_t)sc.verts.size());
+                          sc.mats.data(), sc.sample_textures ? nullptr : sc.tex_albedo.data(),
+                          (uint32_t)sc.mats.size(), sc.tris.data(), (uint32_t)sc.tris.size(), sc.verts.data(),
+                          (uint32_t)sc.verts.size());
 }
 
 int srt_noise_generate(uint32_t texels, int gcc_order, float* noise_rgb, float* noise_uniform_rgb) {

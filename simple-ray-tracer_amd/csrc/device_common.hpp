@@ -16,7 +16,7 @@ using namespace dev;
 struct KParams {
   const float4* nodes;   // node i at nodes[2*i + 2], nodes[2*i + 3]
   const float4* tris;    // 3 float4 per triangle
-  const float4* mats;    // 2 float4 per material
+  const float4* mats;    // 2 float4 per material (m1.w: sampled texture + 1, as bits)
   const float4* lights;  // 2 float4 per light, light_count + 1 records
   const srt_bvh_record* bvhs;
   const float2* noise_xy;
@@ -43,6 +43,11 @@ struct KParams {
   uint32_t* gstack;        // global-scene mode: per-lane stacks in HBM, entry field k of lane g at gstack[k * stride + g]
   int gstack_stride;       // lanes in the grid
   float cx, cy, cz, p00x, p00y, p00z, dux, duy, duz, dvx, dvy, dvz;
+  // texture sampling (the TEX kernel instances)
+  const float4* tri_uv;      // 2 float4 per triangle: vertex uvs uv0 uv1 | uv2
+  const float4* tex_texels;  // RGBA32F texels of all textures
+  const uint4* tex_info;     // per texture: first texel, width, height
+  uint32_t n_tex;
 };
 
 // Dynamic LDS of the path-tracing kernels: [scene copy (LDS mode)] [per-lane stacks].

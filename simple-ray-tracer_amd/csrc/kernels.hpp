@@ -37,7 +37,7 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
 // waves per SIMD the register allocation must allow: 4 (<= 128 VGPRs) in LDS
 // mode, where the 1024-thread block's LDS caps residency at 4 anyway;
 // SRT_GLOBAL_WAVES in global-scene mode, whose HBM latency wants more waves
-template <bool COUNT, bool LDSM, bool PACK, int BLOCK>
+template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX>
 __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_kernel(KParams kp) {
   const int tid = threadIdx.x;
   if constexpr (LDSM) {  // the block copies the scene (nodes + triangles) into LDS once
@@ -242,6 +242,10 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
           const float4 m0 = kp.mats[2 * mi], m1 = kp.mats[2 * mi + 1];
           bump<COUNT>(c, ST_MATS);
           rec.mat.albedo = mk(m0.x, m0.y, m0.z);
+          if constexpr (TEX) {  // the instance for scenes whose materials sample a texture
+            const uint32_t tex = __float_as_uint(m1.w);  // sampled texture + 1
+            if (tex != 0u) rec.mat.albedo = mesh_texture_albedo(kp, tex - 1, ht, A, B, C, dist, ro, rd);
+          }
           rec.mat.roughness = m0.w;
           rec.mat.specular = mk(m1.x, m1.y, m1.z);
           rec.mat.metalness = 0.1f;

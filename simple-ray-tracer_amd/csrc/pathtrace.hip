@@ -80,7 +80,15 @@ struct srt_context {
   uint32_t bvh_uploaded = 0;   // records on the device (valid while !bvhs_dirty)
   bool bvhs_dirty = true;
   std::vector<srt_bvh_record> h_bvhs;
+  std::vector<std::pair<uint32_t, uint32_t>> bvh_tris;  // triangle range [lo, hi) of each record's tree
   uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
+  // textures (srt_upload_textures) and, when materials sample them, the
+  // per-triangle vertex uvs (2 float4: uv0 uv1 | uv2 0 0)
+  float4* d_tex = nullptr;
+  uint4* d_tex_info = nullptr;  // first texel, width, height, 0
+  uint32_t n_tex = 0;
+  float4* d_tri_uv = nullptr;
+  bool sample_textures = false;
   int stack_entries = 1;
   bool scene_ok = false;
   bool lds_ok = false;        // scene indices fit the packed LDS stack entry
@@ -108,7 +116,6 @@ struct srt_context {
   size_t lbuf_bytes = 0;
   size_t lbuf_cap = (size_t)16 << 30;  // SRT_SAMPLE_BUFFER_MB
   int trav_frac16 = 8;                 // SRT_TRAV_FRAC16 (measured best on Rubik 1080p with 2-triangle leaf steps)
-  int lds_block = 1024;                // SRT_LDS_BLOCK (512 or 1024 threads per block in LDS mode)
   int num_cus = 256;
   // stats
   unsigned long long* d_stats = nullptr;
@@ -136,7 +143,26 @@ int EnsureBvhs(srt_context* c) {
   if (!c->bvhs_dirty && c->bvh_uploaded >= need) return SRT_OK;
   std::vector<srt_bvh_record> recs(need);
   std::memset(recs.data(), 0, sizeof(srt_bvh_record) * need);   // bvhs[i >= n] read as zeros
-  for (uint32_t i = 0; i < need && i < c->h_bvhs.size(); ++i) recs[i] = c->h_bvhs[i];
+  for (uint32_t i = 0; i < need && i < c->h_bvhs.size(); ++i) {
+    recs[i] = c->h_bvhs[i];
+    // pad0/pad1 carry the triangle range of the record's tree, empty for a
+    // record whose frame zeroes every direction (it never hits: the ghost
+    // of src/main.cpp:683); texture sampling finds the hit's BVH by it
+    const float* f = recs[i].frame;
+    bool can_hit = false;
+    for (int k : {0, 1, 2, 4, 5, 6, 8, 9, 10}) can_hit = can_hit || f[k] != 0.0f;
+    recs[i].pad0 = can_hit ? c->bvh_tris[i].first : 0u;
+    recs[i].pad1 = can_hit ? c->bvh_tris[i].second : 0u;
+  }
+  if (c->sample_textures) {
+    for (uint32_t i = 0; i < need; ++i)
+      for (uint32_t j = 0; j < i; ++j)
+        if (recs[i].pad0 < recs[i].pad1 && recs[j].pad0 < recs[j].pad1 && recs[i].pad0 < recs[j].pad1 &&
+            recs[j].pad0 < recs[i].pad1) {
+          srt::SetError("texture sampling needs BVH records with disjoint triangle ranges");
+          return SRT_ERR_INVALID;
+        }
+  }
   if (need > c->bvh_capacity) {
     FreeDev(c->d_bvhs);
     c->d_bvhs = nullptr;
@@ -219,6 +245,10 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
   kp->nodes = c->d_nodes;
   kp->tris = c->d_tris;
   kp->mats = c->d_mats;
+  kp->tri_uv = c->d_tri_uv;
+  kp->tex_texels = c->d_tex;
+  kp->tex_info = c->d_tex_info;
+  kp->n_tex = c->d_tex ? c->n_tex : 0u;
   kp->lights = c->d_lights;
   kp->bvhs = c->d_bvhs;
   kp->noise_xy = c->d_noise_xy;
@@ -251,10 +281,10 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
 // LDS budget per CU (gfx950: 160 KiB; one 1024-thread block per CU in LDS mode)
 constexpr size_t kLdsBytes = 160 * 1024;
 
-template <bool COUNT, bool LDSM, bool PACK, int BLOCK>
+template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX>
 int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
   int per_cu = 0;
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sample_kernel<COUNT, LDSM, PACK, BLOCK>, BLOCK,
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX>, BLOCK,
                                                         lds));
   per_cu = std::max(per_cu, 1);
   const int blocks = c->num_cus * per_cu;
@@ -271,9 +301,22 @@ int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
     kp.gstack = c->d_gstack;
     kp.gstack_stride = (int)lanes;
   }
-  hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM, PACK, BLOCK>), dim3(blocks), dim3(BLOCK), lds, c->stream, kp);
+  hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX>), dim3(blocks), dim3(BLOCK), lds, c->stream, kp);
   HIP_OK(hipGetLastError());
   return SRT_OK;
+}
+
+// The sample_kernel instance for the launch: counting or not, LDS-resident
+// scene or global (packed stack entries when indices fit 24 bits), and with
+// or without the texture-sampling branch (TEX, only when a material samples).
+template <bool TEX>
+int LaunchMode(srt_context* c, const srt::KParams& kc, size_t lds, bool count, bool ldsm, bool pack) {
+  if (count && ldsm) return LaunchSamples<true, true, true, 1024, TEX>(c, kc, lds);
+  if (count) return pack ? LaunchSamples<true, false, true, 256, TEX>(c, kc, lds)
+                         : LaunchSamples<true, false, false, 256, TEX>(c, kc, lds);
+  if (ldsm) return LaunchSamples<false, true, true, 1024, TEX>(c, kc, lds);
+  return pack ? LaunchSamples<false, false, true, 256, TEX>(c, kc, lds)
+              : LaunchSamples<false, false, false, 256, TEX>(c, kc, lds);
 }
 
 // Runs frames kp.frame_first .. + kp.nframes - 1 (or the reset frame) through
@@ -290,10 +333,9 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   if (kp.nframes <= 0) return SRT_OK;
   // LDS mode: the whole scene + 1024 lanes' 2-dword stacks fit in one CU's LDS
   const size_t scene_bytes = ((size_t)kp.nodes_f4 + (size_t)kp.tris_f4) * sizeof(float4);
-  const int lds_block = c->lds_block;
-  const size_t lds_mode_bytes = scene_bytes + (size_t)lds_block * 2 * sizeof(uint32_t) * (size_t)kp.stack_entries;
+  const size_t lds_mode_bytes = scene_bytes + (size_t)1024 * 2 * sizeof(uint32_t) * (size_t)kp.stack_entries;
   const bool ldsm = kp.show_model && c->lds_ok && !c->force_global && lds_mode_bytes <= kLdsBytes;
-  const int block = ldsm ? lds_block : 256;
+  const int block = ldsm ? 1024 : 256;
   size_t lds;
   if (ldsm) {
     kp.stack_base_f4 = kp.nodes_f4 + kp.tris_f4;
@@ -346,13 +388,8 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
     HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
     // LDS mode: packed entries (lds_ok); global-scene mode: packed when indices fit 24 bits
     const bool pack = c->lds_ok;
-    if (count && ldsm) rc = block == 512 ? LaunchSamples<true, true, true, 512>(c, kc, lds)
-                                         : LaunchSamples<true, true, true, 1024>(c, kc, lds);
-    else if (count) rc = pack ? LaunchSamples<true, false, true, 256>(c, kc, lds)
-                              : LaunchSamples<true, false, false, 256>(c, kc, lds);
-    else if (ldsm) rc = block == 512 ? LaunchSamples<false, true, true, 512>(c, kc, lds)
-                                     : LaunchSamples<false, true, true, 1024>(c, kc, lds);
-    else rc = pack ? LaunchSamples<false, false, true, 256>(c, kc, lds) : LaunchSamples<false, false, false, 256>(c, kc, lds);
+    rc = c->sample_textures ? LaunchMode<true>(c, kc, lds, count, ldsm, pack)
+                            : LaunchMode<false>(c, kc, lds, count, ldsm, pack);
     if (rc) return rc;
     HIP_OK(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
     c->ev_used += 2;
@@ -379,11 +416,13 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
 
 // Depth of each BVH (root depth 0) and index validation.
 int ValidateNodes(const srt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_tris, const srt_bvh_record* bvhs,
-                  uint32_t n_bvhs, int* max_depth) {
+                  uint32_t n_bvhs, int* max_depth, std::vector<std::pair<uint32_t, uint32_t>>* tri_ranges) {
   *max_depth = 0;
+  tri_ranges->assign(n_bvhs, {0u, 0u});
   std::vector<std::pair<uint32_t, int>> st;
   std::vector<uint8_t> seen(n_nodes, 0);
   for (uint32_t b = 0; b < n_bvhs; ++b) {
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
     if (bvhs[b].first_index >= n_nodes) {
       srt::SetError("BVH first_index out of range");
       return SRT_ERR_INVALID;
@@ -399,6 +438,8 @@ int ValidateNodes(const srt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_tris, 
           srt::SetError("BVH leaf references triangles out of range");
           return SRT_ERR_INVALID;
         }
+        lo = std::min(lo, n.first_child_or_prim_index);
+        hi = std::max(hi, n.first_child_or_prim_index + n.prim_count);
       } else {
         if ((uint64_t)n.first_child_or_prim_index + 1 >= n_nodes || seen[i]) {
           srt::SetError("BVH internal node references children out of range (or a cycle)");
@@ -410,6 +451,7 @@ int ValidateNodes(const srt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_tris, 
       }
     }
     std::fill(seen.begin(), seen.end(), 0);
+    (*tri_ranges)[b] = lo < hi ? std::make_pair(lo, hi) : std::make_pair(0u, 0u);
   }
   return SRT_OK;
 }
@@ -432,7 +474,6 @@ int srt_create(int device, void* stream, srt_context** out) {
   if (const char* e = std::getenv("SRT_FORCE_GLOBAL_SCENE")) c->force_global = e[0] == '1';
   if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_MB")) c->lbuf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
   if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_KB")) c->lbuf_cap = (size_t)std::max(1L, std::atol(e)) << 10;
-  if (const char* e = std::getenv("SRT_LDS_BLOCK")) c->lds_block = std::atoi(e) == 512 ? 512 : 1024;
   if (const char* e = std::getenv("SRT_TRAV_FRAC16")) c->trav_frac16 = std::max(0, std::min(16, std::atoi(e)));
   {
     hipDeviceProp_t prop;
@@ -465,6 +506,7 @@ int srt_destroy(srt_context* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   FreeDev(c->d_nodes); FreeDev(c->d_tris); FreeDev(c->d_mats); FreeDev(c->d_bvhs); FreeDev(c->d_lights);
+  FreeDev(c->d_tex); FreeDev(c->d_tex_info); FreeDev(c->d_tri_uv);
   FreeDev(c->d_noise_xy); FreeDev(c->d_noise_u); FreeDev(c->d_stats); FreeDev(c->d_lbuf); FreeDev(c->d_gstack);
   FreeDev(c->d_batch_ctr);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
@@ -624,7 +666,8 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
     return SRT_ERR_INVALID;
   }
   int depth = 0;
-  int rc = ValidateNodes(nodes, n_nodes, n_tris, bvhs, n_bvhs, &depth);
+  std::vector<std::pair<uint32_t, uint32_t>> tri_ranges;
+  int rc = ValidateNodes(nodes, n_nodes, n_tris, bvhs, n_bvhs, &depth, &tri_ranges);
   if (rc) return rc;
   HIP_OK(hipSetDevice(c->device));
   // nodes: 32-B records behind a 32-B pad so sibling pairs are 64-B aligned
@@ -641,16 +684,25 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   // materials -> shading materials (raytrace_utils.glsl:140-175); one zero
   // record appended for out-of-range material indices (OOB SSBO reads = 0)
   std::vector<float4> hm(2 * ((size_t)n_mats + 1), make_float4(0, 0, 0, 0));
+  bool sampled = false;
   for (uint32_t i = 0; i <= n_mats; ++i) {
     srt_material_obj m{};
     if (i < n_mats) m = mats[i];
     float alb[3] = {m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+    uint32_t tex = 0;  // sampled texture + 1 (0: constant albedo)
     if (m.use_texture) {
       for (int k = 0; k < 3; ++k) alb[k] = tex_albedo ? tex_albedo[3 * (size_t)i + k] : 0.0f;
+      if (!tex_albedo) {
+        const uint64_t h = (uint64_t)m.handle[0] | ((uint64_t)m.handle[1] << 32);
+        tex = h < 0xFFFFFFFFull ? (uint32_t)h + 1 : 0xFFFFFFFFu;  // unknown handles sample zero
+        sampled = true;
+      }
     }
     const float rough = 1.0f / (m.specular_ex + 0.0000001f);
+    float tf;
+    std::memcpy(&tf, &tex, 4);
     hm[2 * (size_t)i] = make_float4(alb[0], alb[1], alb[2], rough);
-    hm[2 * (size_t)i + 1] = make_float4(m.specular[0], m.specular[1], m.specular[2], 0.0f);
+    hm[2 * (size_t)i + 1] = make_float4(m.specular[0], m.specular[1], m.specular[2], tf);
   }
   // triangles: v0, e1 = v1 - v0, e2 = v2 - v0, material
   // kTriPad zero records past the end: a multi-triangle leaf step may read (and discard) them
@@ -671,9 +723,24 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
     ht[3 * (size_t)t + 1] = make_float4(e1[1], e1[2], e2[0], e2[1]);
     ht[3 * (size_t)t + 2] = make_float4(e2[2], mf, 0.0f, 0.0f);
   }
-  FreeDev(c->d_nodes); FreeDev(c->d_mats); FreeDev(c->d_tris);
-  c->d_nodes = nullptr; c->d_mats = nullptr; c->d_tris = nullptr;
+  // vertex uvs per triangle, for the materials that sample a texture
+  std::vector<float4> huv;
+  if (sampled) {
+    huv.assign(2 * (size_t)n_tris, make_float4(0, 0, 0, 0));
+    auto uv = [&](uint32_t i, int k) -> float { return i < n_verts ? verts[i].texture[k] : 0.0f; };
+    for (uint32_t t = 0; t < n_tris; ++t) {
+      const srt_triangle& tr = tris[t];
+      huv[2 * (size_t)t] = make_float4(uv(tr.v0_idx, 0), uv(tr.v0_idx, 1), uv(tr.v1_idx, 0), uv(tr.v1_idx, 1));
+      huv[2 * (size_t)t + 1] = make_float4(uv(tr.v2_idx, 0), uv(tr.v2_idx, 1), 0.0f, 0.0f);
+    }
+  }
+  FreeDev(c->d_nodes); FreeDev(c->d_mats); FreeDev(c->d_tris); FreeDev(c->d_tri_uv);
+  c->d_nodes = nullptr; c->d_mats = nullptr; c->d_tris = nullptr; c->d_tri_uv = nullptr;
   c->scene_ok = false;
+  if (sampled && n_tris) {
+    HIP_OK(hipMalloc(&c->d_tri_uv, huv.size() * sizeof(float4)));
+    HIP_OK(hipMemcpyAsync(c->d_tri_uv, huv.data(), huv.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+  }
   HIP_OK(hipMalloc(&c->d_nodes, hn.size() * sizeof(float4)));
   HIP_OK(hipMalloc(&c->d_mats, hm.size() * sizeof(float4)));
   HIP_OK(hipMalloc(&c->d_tris, ht.size() * sizeof(float4)));
@@ -682,6 +749,8 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   HIP_OK(hipMemcpyAsync(c->d_tris, ht.data(), ht.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
   c->h_bvhs.assign(bvhs, bvhs + n_bvhs);
+  c->bvh_tris = std::move(tri_ranges);
+  c->sample_textures = sampled;
   c->bvhs_dirty = true;
   c->n_nodes = n_nodes;
   c->n_tris = n_tris;
@@ -694,6 +763,48 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   if (c->bvh_count == 0) c->bvh_count = n_bvhs;
   // the zero records beyond n_bvhs traverse from node 0 with a zero ray
   // (raytrace_compute.glsl:144-147 reading bvhs[i] out of bounds)
+  return SRT_OK;
+}
+
+int srt_upload_textures(srt_context* c, const srt_texture* textures, uint32_t n) {
+  if (!c || (n && !textures)) return SRT_ERR_INVALID;
+  std::vector<uint4> info(std::max<uint32_t>(n, 1), make_uint4(0, 0, 0, 0));
+  size_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const srt_texture& t = textures[i];
+    if (!t.texels || t.width <= 0 || t.height <= 0 || t.channels < 1 || t.channels > 4) {
+      srt::SetError("texture " + std::to_string(i) + ": bad size, channel count or texel pointer");
+      return SRT_ERR_INVALID;
+    }
+    info[i] = make_uint4((uint32_t)total, (uint32_t)t.width, (uint32_t)t.height, 0u);
+    total += (size_t)t.width * (size_t)t.height;
+    if (total >= (1ull << 32)) {
+      srt::SetError("textures hold more than 2^32 texels");
+      return SRT_ERR_LIMIT;
+    }
+  }
+  // RGBA32F texels, c / 255 (unorm8); GL_RED reads (r, 0, 0), a 2-channel file (r, g, 0)
+  std::vector<float4> tx(std::max<size_t>(total, 1), make_float4(0, 0, 0, 0));
+  for (uint32_t i = 0; i < n; ++i) {
+    const srt_texture& t = textures[i];
+    const size_t m = (size_t)t.width * (size_t)t.height;
+    for (size_t k = 0; k < m; ++k) {
+      const uint8_t* p = t.texels + k * t.channels;
+      float v[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+      for (int ch = 0; ch < t.channels && ch < 3; ++ch) v[ch] = (float)p[ch] / 255.0f;
+      if (t.channels == 2) v[2] = 0.0f;
+      tx[info[i].x + k] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+  HIP_OK(hipSetDevice(c->device));
+  FreeDev(c->d_tex); FreeDev(c->d_tex_info);
+  c->d_tex = nullptr; c->d_tex_info = nullptr; c->n_tex = 0;
+  HIP_OK(hipMalloc(&c->d_tex, tx.size() * sizeof(float4)));
+  HIP_OK(hipMalloc(&c->d_tex_info, info.size() * sizeof(uint4)));
+  HIP_OK(hipMemcpyAsync(c->d_tex, tx.data(), tx.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipMemcpyAsync(c->d_tex_info, info.data(), info.size() * sizeof(uint4), hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  c->n_tex = n;
   return SRT_OK;
 }
 

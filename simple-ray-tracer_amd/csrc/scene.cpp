@@ -51,6 +51,8 @@ bool ReadFloat(std::istringstream& ls, float* out) {
 
 struct Face {
   uint32_t v[3];
+  uint32_t t[3] = {0, 0, 0};  // vt indices, valid when t_ok (IsTextureIdxsValid)
+  bool t_ok = false;
 };
 
 struct SubGeometry {
@@ -59,8 +61,19 @@ struct SubGeometry {
 };
 
 // model_loader.cpp:35-177 ParseOBJ
-bool ParseOBJ(const std::string& path, std::vector<Vec3>* vertices, std::vector<SubGeometry>* geos,
-              std::vector<std::string>* mtl_files, uint64_t* dropped, std::string* err) {
+bool ParseOBJ(const std::string& path, std::vector<Vec3>* vertices, std::vector<std::pair<float, float>>* uvs,
+              std::vector<SubGeometry>* geos, std::vector<std::string>* mtl_files, uint64_t* dropped,
+              std::string* err) {
+  auto index = [&](const std::string& tok, uint32_t* out) {
+    char* end = nullptr;
+    const long idx = std::strtol(tok.c_str(), &end, 10);
+    if (end == tok.c_str()) {
+      *err = "bad face index '" + tok + "' in " + path;
+      return false;  // std::stol throws in the reference
+    }
+    *out = static_cast<uint32_t>(idx - 1);  // OBJ indices are 1-based
+    return true;
+  };
   std::ifstream file(path);
   if (!file) {
     *err = "cannot open " + path;
@@ -77,28 +90,48 @@ bool ParseOBJ(const std::string& path, std::vector<Vec3>* vertices, std::vector<
     if (prefix == "v") {
       Vec3 v;
       if (ReadFloat(ls, &v.x) && ReadFloat(ls, &v.y) && ReadFloat(ls, &v.z)) vertices->push_back(v);
-    } else if (prefix == "f") {
-      std::vector<uint32_t> vi;
+    } else if (prefix == "vt") {  // model_loader.cpp:65-71
+      float a, b;
+      if (ReadFloat(ls, &a) && ReadFloat(ls, &b)) uvs->emplace_back(a, b);
+    } else if (prefix == "f") {  // model_loader.cpp:82-143: v/vt/vn per corner
+      std::vector<uint32_t> vi, ti;
       std::string tok;
       while (ls >> tok) {
-        const auto slash = tok.find('/');
-        const std::string v = tok.substr(0, slash);
+        const auto s1 = tok.find('/');
+        const std::string v = tok.substr(0, s1);
+        std::string vt;
+        if (s1 != std::string::npos) {
+          const auto s2 = tok.find('/', s1 + 1);
+          vt = tok.substr(s1 + 1, s2 == std::string::npos ? std::string::npos : s2 - s1 - 1);
+        }
+        uint32_t idx;
         if (!v.empty()) {
-          char* end = nullptr;
-          long idx = std::strtol(v.c_str(), &end, 10);
-          if (end == v.c_str()) {
-            *err = "bad face index '" + v + "' in " + path;
-            return false;  // std::stol throws in the reference
-          }
-          vi.push_back(static_cast<uint32_t>(idx - 1));  // OBJ indices are 1-based
+          if (!index(v, &idx)) return false;
+          vi.push_back(idx);
+        }
+        if (!vt.empty()) {
+          if (!index(vt, &idx)) return false;
+          ti.push_back(idx);
         }
       }
       if (vi.size() != 3 && vi.size() != 4) {
         ++*dropped;  // "Unexpected face vertex count" (model_loader.cpp:110-113)
         continue;
       }
-      cur.faces.push_back(Face{{vi[0], vi[1], vi[2]}});
-      if (vi.size() == 4) cur.faces.push_back(Face{{vi[0], vi[2], vi[3]}});
+      Face f1{{vi[0], vi[1], vi[2]}};
+      if (ti.size() > 2) {
+        f1.t[0] = ti[0]; f1.t[1] = ti[1]; f1.t[2] = ti[2];
+        f1.t_ok = true;
+      }
+      cur.faces.push_back(f1);
+      if (vi.size() == 4) {
+        Face f2{{vi[0], vi[2], vi[3]}};
+        if (ti.size() == 4) {
+          f2.t[0] = ti[0]; f2.t[1] = ti[2]; f2.t[2] = ti[3];
+          f2.t_ok = true;
+        }
+        cur.faces.push_back(f2);
+      }
     } else if (prefix == "usemtl") {
       if (!cur.material.empty()) {
         geos->push_back(std::move(cur));
@@ -112,8 +145,7 @@ bool ParseOBJ(const std::string& path, std::vector<Vec3>* vertices, std::vector<
       ls >> name;
       mtl_files->push_back(name);
     }
-    // vt / vn are parsed by the reference but never reach the GPU (has_texcoords
-    // is never set, types.h:105); s / o / g and unknown prefixes are ignored.
+    // vn never reaches the GPU; s / o / g and unknown prefixes are ignored.
   }
   if (!cur.material.empty()) geos->push_back(std::move(cur));
   else *dropped += cur.faces.size();  // trailing faces without a material are dropped
@@ -524,25 +556,40 @@ bool DecodePng(const std::string& path, int* w, int* h, int* ch, std::vector<uns
 
 }  // namespace
 
-// texture(sampler2D, vec2(0)) at level 0 with GL_REPEAT + GL_LINEAR: the four
-// corner texels, weight 1/4 each (gpu_texture.h:24-68 uploads stb_image rows).
-bool DecodeTextureCornerAlbedo(const std::string& path, Vec3* out, std::string* err) {
-  int w = 0, h = 0, ch = 0;
-  std::vector<unsigned char> px;
-  if (!DecodePng(path, &w, &h, &ch, &px, err)) return false;
-  auto texel = [&](int x, int y) -> Vec3 {
-    const unsigned char* p = &px[(size_t(y) * w + x) * ch];
-    // GL_RED (1 ch) samples as (r,0,0); 2-channel falls back to GL_RGB in the
-    // reference's format switch, reading (r,g,?) -- treated as (r,g,0).
-    float r = p[0] / 255.0f;
-    float g = ch >= 2 ? p[1] / 255.0f : 0.0f;
-    float b = ch >= 3 ? p[2] / 255.0f : 0.0f;
-    return Vec3(r, g, b);
+bool DecodePngTexture(const std::string& path, Texture* out, std::string* err) {
+  out->path = path;
+  return DecodePng(path, &out->width, &out->height, &out->channels, &out->texels, err);
+}
+
+// texture(sampler2D, vec2(s, t)) at level 0 with GL_LINEAR + GL_REPEAT
+// (gpu_texture.h:52-58; a compute shader has no derivatives, so lod = 0 and
+// the magnification filter applies).  The contract, shared with the kernel
+// (shading.hpp texture_sample) and the oracle: fp32 in source order, a
+// non-finite coordinate reads as 0, REPEAT as s - floor(s), texel centres at
+// (i + 0.5) / size, texels c / 255, and the four weighted texels summed
+// (00 + 10) + 01 + 11.  GL_RED samples as (r, 0, 0); a 2-channel file, which
+// the reference uploads as GL_RGB, as (r, g, 0).
+void TextureSample(const uint8_t* texels, int width, int height, int channels, float s, float t, float rgb[3]) {
+  if (!(std::fabs(s) <= 3.402823466e38f)) s = 0.0f;
+  if (!(std::fabs(t) <= 3.402823466e38f)) t = 0.0f;
+  s = s - std::floor(s);
+  t = t - std::floor(t);
+  const float x = s * (float)width - 0.5f, y = t * (float)height - 0.5f;
+  const float fx = std::floor(x), fy = std::floor(y);
+  const float a = x - fx, b = y - fy;
+  int i0 = (int)fx, j0 = (int)fy;
+  int i1 = i0 + 1, j1 = j0 + 1;
+  i0 = i0 < 0 ? width - 1 : i0;
+  j0 = j0 < 0 ? height - 1 : j0;
+  i1 = i1 >= width ? 0 : i1;
+  j1 = j1 >= height ? 0 : j1;
+  const float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+  auto texel = [&](int i, int j, int k) -> float {
+    if (k >= channels || (k == 2 && channels == 2)) return 0.0f;
+    return (float)texels[((size_t)j * width + i) * channels + k] / 255.0f;
   };
-  const Vec3 a = texel(0, 0), b = texel(w - 1, 0), c = texel(0, h - 1), d = texel(w - 1, h - 1);
-  *out = Vec3(0.25f * (((a.x + b.x) + c.x) + d.x), 0.25f * (((a.y + b.y) + c.y) + d.y),
-              0.25f * (((a.z + b.z) + c.z) + d.z));
-  return true;
+  for (int k = 0; k < 3; ++k)
+    rgb[k] = ((w00 * texel(i0, j0, k) + w10 * texel(i1, j0, k)) + w01 * texel(i0, j1, k)) + w11 * texel(i1, j1, k);
 }
 
 int BvhThreads() {
@@ -553,20 +600,36 @@ int BvhThreads() {
 void BuildBVH(Model* m) { BvhBuilder(m, BvhThreads()).Build(); }
 
 // model_loader.cpp:20-32 + 280-365
-std::unique_ptr<Model> LoadObjectFile(const std::string& obj_path, std::string* err) {
+std::unique_ptr<Model> LoadObjectFile(const std::string& obj_path, bool texcoords, std::string* err) {
   std::vector<Vec3> vertices;
+  std::vector<std::pair<float, float>> uvs;
   std::vector<SubGeometry> geos;
   std::vector<std::string> mtl_files;
   auto model = std::make_unique<Model>();
-  if (!ParseOBJ(obj_path, &vertices, &geos, &mtl_files, &model->faces_dropped, err)) return nullptr;
+  model->texcoords = texcoords;
+  if (!ParseOBJ(obj_path, &vertices, &uvs, &geos, &mtl_files, &model->faces_dropped, err)) return nullptr;
   const auto slash = obj_path.find_last_of('/');
   const std::string folder = slash == std::string::npos ? std::string("./") : obj_path.substr(0, slash + 1);
   std::vector<std::string> names;
   for (const auto& f : mtl_files) ParseMTL(folder, f, &names, &model->materials);
+  // one decoded texture per file (the reference's LoadedTextures cache, gpu_texture.h:20-28)
   for (auto& m : model->materials) {
-    if (m.use_texture && !DecodeTextureCornerAlbedo(m.texture_path, &m.tex_albedo, err)) return nullptr;
+    if (!m.use_texture) continue;
+    for (size_t k = 0; k < model->textures.size(); ++k)
+      if (model->textures[k].path == m.texture_path) m.texture = (int)k;
+    if (m.texture < 0) {
+      Texture tex;
+      if (!DecodePngTexture(m.texture_path, &tex, err)) return nullptr;
+      model->textures.push_back(std::move(tex));
+      m.texture = (int)model->textures.size() - 1;
+    }
+    const Texture& tx = model->textures[m.texture];
+    float rgb[3];
+    TextureSample(tx.texels.data(), tx.width, tx.height, tx.channels, 0.0f, 0.0f, rgb);
+    m.tex_albedo = Vec3(rgb[0], rgb[1], rgb[2]);
   }
   // per-corner vertex duplication (model_loader.cpp:302-331); uv stays (0,0)
+  // unless texcoords (has_texcoords, never set by the reference)
   for (const auto& g : geos) {
     uint32_t mat = 0;
     for (size_t k = 0; k < names.size(); ++k)
@@ -582,6 +645,14 @@ std::unique_ptr<Model> LoadObjectFile(const std::string& obj_path, std::string* 
         const Vec3& p = vertices[f.v[c]];
         srt_vertex sv{};
         sv.vertex[0] = p.x; sv.vertex[1] = p.y; sv.vertex[2] = p.z;
+        if (texcoords && f.t_ok) {
+          if (f.t[c] >= uvs.size()) {
+            *err = "face references texcoord " + std::to_string(f.t[c] + 1) + " out of range";
+            return nullptr;
+          }
+          sv.texture[0] = uvs[f.t[c]].first;
+          sv.texture[1] = uvs[f.t[c]].second;
+        }
         model->vertices.push_back(sv);
         t.vertex_idxs[c] = static_cast<uint32_t>(model->vertices.size() - 1);
       }
@@ -631,12 +702,16 @@ std::unique_ptr<Scene> FlattenModels(const std::vector<const Model*>& models, st
       return nullptr;
     }
     const uint32_t model_mat_off = mat_off;
+    const uint32_t model_tex_off = static_cast<uint32_t>(s->textures.size());
+    s->textures.insert(s->textures.end(), m->textures.begin(), m->textures.end());
+    s->sample_textures = s->sample_textures || (m->texcoords && !m->textures.empty());
     for (const auto& mat : m->materials) {
       srt_material_obj g{};
       g.diffuse[0] = mat.diffuse.x; g.diffuse[1] = mat.diffuse.y; g.diffuse[2] = mat.diffuse.z;
       g.specular[0] = mat.specular.x; g.specular[1] = mat.specular.y; g.specular[2] = mat.specular.z;
       g.specular_ex = mat.specular_ex;
       g.use_texture = mat.use_texture ? 1u : 0u;
+      if (mat.use_texture) g.handle[0] = model_tex_off + static_cast<uint32_t>(mat.texture);
       s->mats.push_back(g);
       s->tex_albedo.push_back(mat.tex_albedo.x);
       s->tex_albedo.push_back(mat.tex_albedo.y);

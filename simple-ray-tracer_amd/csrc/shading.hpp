@@ -3,9 +3,66 @@
 #pragma once
 
 #include "device_common.hpp"
+#include "traversal.hpp"
 
 namespace srt {
 using namespace dev;
+
+// texture(sampler2D, vec2(s, t)).xyz at level 0, GL_LINEAR, GL_REPEAT: the
+// sampling contract of scene.cpp TextureSample
+__device__ __forceinline__ f3 texture_sample(const KParams& kp, uint32_t tex, float s, float t) {
+  const uint4 info = kp.tex_info[tex];
+  const int w = (int)info.y, h = (int)info.z;
+  if (!(__builtin_fabsf(s) <= 3.402823466e38f)) s = 0.0f;
+  if (!(__builtin_fabsf(t) <= 3.402823466e38f)) t = 0.0f;
+  s = s - __builtin_floorf(s);
+  t = t - __builtin_floorf(t);
+  const float x = s * (float)w - 0.5f, y = t * (float)h - 0.5f;
+  const float fx = __builtin_floorf(x), fy = __builtin_floorf(y);
+  const float a = x - fx, b = y - fy;
+  int i0 = (int)fx, j0 = (int)fy;
+  int i1 = i0 + 1, j1 = j0 + 1;
+  i0 = i0 < 0 ? w - 1 : i0;
+  j0 = j0 < 0 ? h - 1 : j0;
+  i1 = i1 >= w ? 0 : i1;
+  j1 = j1 >= h ? 0 : j1;
+  const float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+  const float4* T = kp.tex_texels + info.x;
+  const float4 t00 = T[(uint32_t)j0 * w + i0], t10 = T[(uint32_t)j0 * w + i1];
+  const float4 t01 = T[(uint32_t)j1 * w + i0], t11 = T[(uint32_t)j1 * w + i1];
+  return mk(((w00 * t00.x + w10 * t10.x) + w01 * t01.x) + w11 * t11.x,
+            ((w00 * t00.y + w10 * t10.y) + w01 * t01.y) + w11 * t11.y,
+            ((w00 * t00.z + w10 * t10.z) + w01 * t01.z) + w11 * t11.z);
+}
+
+// TriangleToSupportedMat's texture branch (raytrace_utils.glsl:144-166) for
+// hit triangle `ht` (records A, B, C: v0, e1 = v1 - v0, e2 = v2 - v0) at
+// distance `dist` along the world ray: model_p in the frame of the BVH that
+// owns the triangle (raytrace_compute.glsl:155), barycentrics, uv, sample.
+__device__ __forceinline__ f3 mesh_texture_albedo(const KParams& kp, uint32_t tex, uint32_t ht, float4 A, float4 B,
+                                               float4 C, float dist, f3 ro, f3 rd) {
+  if (tex >= kp.n_tex) return mk(0.0f, 0.0f, 0.0f);  // unknown handle
+  uint32_t hb = 0;
+  for (uint32_t j = 0; j < kp.bvh_count; ++j) {  // pad0/pad1: the record's triangle range
+    const srt_bvh_record& r = kp.bvhs[j];
+    if (ht - r.pad0 < r.pad1 - r.pad0) hb = j;
+  }
+  const srt_bvh_record& b = kp.bvhs[hb];
+  const f3 to = xform(b.frame, ro, 1.0f), td = xform(b.frame, rd, 0.0f);
+  const f3 mp = (dist * td) + to;
+  const f3 v0 = mk(A.x, A.y, A.z), v0v1 = mk(A.w, B.x, B.y), v0v2 = mk(B.z, B.w, C.x);
+  const f3 v0p = mp - v0;
+  const float d00 = dot(v0v1, v0v1), d01 = dot(v0v1, v0v2), d11 = dot(v0v2, v0v2);
+  const float d20 = dot(v0p, v0v1), d21 = dot(v0p, v0v2);
+  const float denom = 1.0f / (d00 * d11 - d01 * d01);
+  const float v = (d11 * d20 - d01 * d21) * denom;
+  const float w = (d00 * d21 - d01 * d20) * denom;
+  const float u = 1.0f - v - w;
+  const float4 uv01 = kp.tri_uv[2 * ht], uv2 = kp.tri_uv[2 * ht + 1];
+  const float s = (u * uv01.x + v * uv01.z) + w * uv2.x;
+  const float t = (u * uv01.y + v * uv01.w) + w * uv2.y;
+  return texture_sample(kp, tex, s, t);
+}
 
 // raytrace_compute.glsl:93-120 SphereHit
 __device__ __forceinline__ bool sphere_hit(f3 ro, f3 rd, f3 pos, float radius, float mn, float mx, float& t) {

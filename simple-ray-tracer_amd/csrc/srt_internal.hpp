@@ -42,14 +42,22 @@ struct Triangle {
   uint32_t material_idx;
 };
 
-// asset_utils/types.h:31-37 (texture decoded to its uv=(0,0) sample at load)
+// A decoded map_Kd texture in stb_image layout (gpu_texture.h:29-33)
+struct Texture {
+  std::string path;
+  int width = 0, height = 0, channels = 0;
+  std::vector<uint8_t> texels;  // rows top first, `channels` bytes per texel
+};
+
+// asset_utils/types.h:31-37
 struct Material {
   Vec3 diffuse;
   Vec3 specular;
   float specular_ex = 0.f;
   bool use_texture = false;
   std::string texture_path;
-  Vec3 tex_albedo;  // texture(sampler2D(handle), (0,0)).xyz
+  int texture = -1;  // index into Model::textures
+  Vec3 tex_albedo;   // texture(sampler2D(handle), (0,0)).xyz: the albedo while every uv is (0,0)
 };
 
 // asset_utils/types.h:39-52
@@ -58,6 +66,8 @@ struct Model {
   std::vector<Triangle> prims;         // BVH-ordered
   std::vector<Material> materials;
   std::vector<srt_vertex> vertices;    // PackedVertexData, 32 B
+  std::vector<Texture> textures;       // one per distinct map_Kd file
+  bool texcoords = false;              // loaded with SRT_LOAD_TEXCOORDS
   uint64_t faces_dropped = 0;
   uint32_t max_depth = 0;
   uint32_t leaves = 0;
@@ -71,15 +81,19 @@ struct Scene {
   std::vector<float> tex_albedo;       // 3 per material
   std::vector<srt_triangle> tris;
   std::vector<srt_vertex> verts;
+  std::vector<Texture> textures;         // material handle = index
+  bool sample_textures = false;          // some model carries real uvs
 };
 
 // producers (scene.cpp)
-std::unique_ptr<Model> LoadObjectFile(const std::string& obj_path, std::string* err);
+std::unique_ptr<Model> LoadObjectFile(const std::string& obj_path, bool texcoords, std::string* err);
 std::unique_ptr<Model> ModelFromTriangles(const float* xyz9, uint32_t n, const Vec3& kd, const Vec3& ks,
                                           float ns);
 void BuildBVH(Model* m);  // bvh.h:40-75 over m->prims with the loader's centre/bounds functions
 std::unique_ptr<Scene> FlattenModels(const std::vector<const Model*>& models, std::string* err);
-bool DecodeTextureCornerAlbedo(const std::string& path, Vec3* out, std::string* err);
+bool DecodePngTexture(const std::string& path, Texture* out, std::string* err);
+// texture(sampler2D, vec2(s, t)).xyz under the sampling contract
+void TextureSample(const uint8_t* texels, int width, int height, int channels, float s, float t, float rgb[3]);
 
 // noise.cpp
 void GlibcRand(uint32_t n, int32_t* out);

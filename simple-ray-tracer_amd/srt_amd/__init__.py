@@ -178,10 +178,28 @@ class Model:
             self._h = None
 
 
-def load_obj(obj_path: str | pathlib.Path) -> Model:
+SRT_LOAD_TEXCOORDS = 1
+
+
+def load_obj(obj_path: str | pathlib.Path, texcoords: bool = False) -> Model:
+    """LoadObject's parser on one .obj path.  ``texcoords=True`` gives vertices their ``vt`` uvs (the loader
+    with has_texcoords set, model_loader.cpp:322-324); the reference leaves every uv at (0,0)."""
     h = C.c_void_p()
-    check(lib().srt_model_load(str(obj_path).encode(), C.byref(h)), f"LoadObject({obj_path})")
+    flags = SRT_LOAD_TEXCOORDS if texcoords else 0
+    check(lib().srt_model_load_ex(str(obj_path).encode(), flags, C.byref(h)), f"LoadObject({obj_path})")
     return Model(h.value)
+
+
+def texture_sample(texels: np.ndarray, s: float, t: float) -> np.ndarray:
+    """texture(sampler2D, vec2(s, t)).xyz on the host (the sampling contract, DESIGN.md section 3);
+    ``texels`` is (H, W, C) uint8, rows top first."""
+    tex = np.ascontiguousarray(texels, np.uint8)
+    if tex.ndim == 2:
+        tex = tex[:, :, None]
+    desc = _lib.Texture(tex.ctypes.data, tex.shape[1], tex.shape[0], tex.shape[2])
+    out = np.zeros(3, np.float32)
+    check(lib().srt_texture_sample(C.byref(desc), C.c_float(s), C.c_float(t), _ptr(out)), "texture_sample")
+    return out
 
 
 def LoadObject(name: str, objects_dir: str | pathlib.Path = "./objects/") -> Model:
@@ -208,6 +226,8 @@ class Scene:
     tex_albedo: np.ndarray
     tris: np.ndarray
     verts: np.ndarray
+    textures: list = field(default_factory=list)  # (H, W, C) uint8 per texture handle
+    sample_textures: bool = False                  # sample at the hit's uv instead of tex_albedo
 
     @classmethod
     def from_models(cls, models: Sequence[Model | None]) -> "Scene":
@@ -221,6 +241,15 @@ class Scene:
                     np.zeros((sizes[2], 3), np.float32), np.zeros(sizes[3], TRI_DTYPE), np.zeros(sizes[4], VERT_DTYPE))
             check(lib().srt_scene_copy(sh, _ptr(s.bvhs), _ptr(s.nodes), _ptr(s.mats), _ptr(s.tex_albedo),
                                        _ptr(s.tris), _ptr(s.verts)), "srt_scene_copy")
+            n, sample = C.c_uint32(), C.c_int()
+            check(lib().srt_scene_texture_count(sh, C.byref(n), C.byref(sample)), "srt_scene_texture_count")
+            for i in range(n.value):
+                t = _lib.Texture()
+                check(lib().srt_scene_texture(sh, i, C.byref(t)), "srt_scene_texture")
+                nbytes = t.width * t.height * t.channels
+                buf = (C.c_uint8 * nbytes).from_address(t.texels)
+                s.textures.append(np.frombuffer(buf, np.uint8).copy().reshape(t.height, t.width, t.channels))
+            s.sample_textures = bool(sample.value)
         finally:
             lib().srt_scene_free(sh)
         return s
@@ -330,11 +359,21 @@ class Compute:
         arr = np.ascontiguousarray(arr, dtype=LIGHT_DTYPE)
         check(lib().srt_set_lights(self.ctx, _ptr(arr), len(arr)), "bind_lights")
 
+    def bind_textures(self, textures: Sequence[np.ndarray]):
+        """GPUTexture + GetHandle for each (H, W, C) uint8 texture: texture i gets handle i."""
+        keep = [np.ascontiguousarray(t if t.ndim == 3 else t[:, :, None], np.uint8) for t in textures]
+        descs = (_lib.Texture * max(len(keep), 1))(*[_lib.Texture(t.ctypes.data, t.shape[1], t.shape[0], t.shape[2])
+                                                      for t in keep])
+        check(lib().srt_upload_textures(self.ctx, descs, len(keep)), "bind_textures")
+
     def bind_scene(self, scene: Scene):
         s = scene
+        if s.sample_textures:
+            self.bind_textures(s.textures)
+        tex = None if s.sample_textures else np.ascontiguousarray(s.tex_albedo, np.float32)
         check(lib().srt_upload_scene(self.ctx, _ptr(s.bvhs), len(s.bvhs), _ptr(s.nodes), len(s.nodes),
-                                     _ptr(s.mats), _ptr(np.ascontiguousarray(s.tex_albedo, np.float32)),
-                                     len(s.mats), _ptr(s.tris), len(s.tris), _ptr(s.verts), len(s.verts)),
+                                     _ptr(s.mats), _ptr(tex), len(s.mats), _ptr(s.tris), len(s.tris), _ptr(s.verts),
+                                     len(s.verts)),
               "UploadModelDataToGPU")
 
     def set_tiling(self, rank: int, nranks: int, band_rows: int = 16):

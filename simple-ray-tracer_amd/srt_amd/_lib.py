@@ -66,6 +66,10 @@ class Stats(C.Structure):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
 
 
+class Texture(C.Structure):
+    _fields_ = [("texels", C.c_void_p), ("width", C.c_int32), ("height", C.c_int32), ("channels", C.c_int32)]
+
+
 assert C.sizeof(BvhRecord) == 80 and C.sizeof(BvhNode) == 32 and C.sizeof(MaterialObj) == 48
 assert C.sizeof(Triangle) == 16 and C.sizeof(Vertex) == 32 and C.sizeof(Light) == 32 and C.sizeof(Ray) == 32
 
@@ -91,6 +95,8 @@ _SIGS = {
     "srt_local_rows": (C.c_int, [P]),
     "srt_upload_scene": (C.c_int, [P, P, C.c_uint32, P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P,
                                    C.c_uint32]),
+    "srt_upload_textures": (C.c_int, [P, C.POINTER(Texture), C.c_uint32]),
+    "srt_texture_sample": (C.c_int, [C.POINTER(Texture), C.c_float, C.c_float, P]),
     "srt_update_model_matrix": (C.c_int, [P, C.c_uint32, P]),
     "srt_set_lights": (C.c_int, [P, P, C.c_uint32]),
     "srt_set_noise": (C.c_int, [P, P, P, C.c_size_t]),
@@ -105,6 +111,7 @@ _SIGS = {
     "srt_assemble_bands": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
     "srt_trace_closest": (C.c_int, [P, P, C.c_uint32, P, P]),
     "srt_model_load": (C.c_int, [C.c_char_p, C.POINTER(P)]),
+    "srt_model_load_ex": (C.c_int, [C.c_char_p, C.c_uint32, C.POINTER(P)]),
     "srt_model_from_triangles": (C.c_int, [P, C.c_uint32, P, P, C.c_float, C.POINTER(P)]),
     "srt_model_free": (C.c_int, [P]),
     "srt_model_info": (C.c_int, [P, P, P, P]),
@@ -112,6 +119,8 @@ _SIGS = {
     "srt_scene_free": (C.c_int, [P]),
     "srt_scene_sizes": (C.c_int, [P, P]),
     "srt_scene_copy": (C.c_int, [P, P, P, P, P, P, P]),
+    "srt_scene_texture_count": (C.c_int, [P, C.POINTER(C.c_uint32), C.POINTER(C.c_int)]),
+    "srt_scene_texture": (C.c_int, [P, C.c_uint32, C.POINTER(Texture)]),
     "srt_upload_scene_obj": (C.c_int, [P, P]),
     "srt_noise_generate": (C.c_int, [C.c_uint32, C.c_int, P, P]),
     "srt_glibc_rand": (C.c_int, [C.c_uint32, P]),

@@ -134,6 +134,55 @@ def test_textured_material_albedo(tmp_path):
     assert_parity(setup, 2)
 
 
+def _textured_obj(tmp_path):
+    """Two textured quads (RGB and single-channel PNGs) whose vt coordinates leave [0,1], so REPEAT wraps."""
+    import test_producers as P
+
+    rng = np.random.default_rng(7)
+    P._write_png(tmp_path / "a.png", 8, 6, [int(x) for x in rng.integers(0, 256, 8 * 6 * 3)])
+    P._write_png(tmp_path / "b.png", 5, 3, [int(x) for x in rng.integers(0, 256, 5 * 3)], ctype=0)
+    (tmp_path / "m.mtl").write_text("newmtl a\nKd 1 1 1\nKs 0.3 0.3 0.3\nNs 30\nmap_Kd a.png\n"
+                                    "newmtl b\nKd 1 1 1\nKs 0.1 0.1 0.1\nNs 5\nmap_Kd b.png\n")
+    (tmp_path / "m.obj").write_text(
+        "mtllib m.mtl\n"
+        "v -20 -2 -6\nv 20 -2 -6\nv 20 28 -6\nv -20 28 -6\nv -20 -2 25\nv 20 -2 25\n"
+        "vt -1.3 -0.7\nvt 2.6 -0.7\nvt 2.6 2.7\nvt -1.3 2.7\nvt 0.25 3.5\nvt 4.75 3.5\n"
+        "usemtl a\nf 1/1 2/2 3/3 4/4\n"
+        "usemtl b\nf 5/5 6/6 2/2 1/1\n")
+    return tmp_path / "m.obj"
+
+
+def test_sampled_texture_parity(tmp_path):
+    """textures sampled at the hit's interpolated uv (loader with has_texcoords set)."""
+    setup = R.make_setup(48, 40, show_model=True, models=[S.load_obj(_textured_obj(tmp_path), texcoords=True)])
+    assert setup.scene.sample_textures and len(setup.scene.textures) == 2
+    assert_parity(setup, 3)
+
+
+def test_sampled_texture_at_zero_uv_is_the_constant_albedo(tmp_path):
+    """With the reference's loader every uv is (0,0): sampling per hit gives the precomputed tex_albedo, bit for bit."""
+    import dataclasses
+
+    setup = R.make_setup(48, 40, show_model=True, models=[S.load_obj(_textured_obj(tmp_path))])
+    assert not setup.scene.sample_textures
+    a, o, _ = gpu_render(setup, 3)
+    sampled = dataclasses.replace(setup, scene=dataclasses.replace(setup.scene, sample_textures=True))
+    b, p, _ = gpu_render(sampled, 3)
+    assert bits_equal(a, b).all() and (o == p).all()
+
+
+def test_sampled_texture_two_models_with_transform(tmp_path):
+    """The hit's model-space point comes from the frame of the BVH that owns the triangle; a ghost record
+    (bvh_count beyond the models) never hits."""
+    obj = _textured_obj(tmp_path)
+    setup = R.make_setup(48, 40, show_model=True, models=[S.load_obj(obj, texcoords=True),
+                                                          S.load_obj(obj, texcoords=True)], bvh_count=3)
+    frame = np.eye(4, dtype=np.float32)
+    frame[3, :3] = (4.0, -3.0, 7.0)
+    setup.scene.bvhs[1]["frame"] = frame.reshape(16)
+    assert_parity(setup, 2)
+
+
 def test_synthetic_mesh_global_mode():
     """A 30k-triangle mesh: too big for the LDS copy, exercises the global-memory traversal."""
     setup = R.make_setup(40, 30, show_model=True, models=[R.synthetic_model(30000, seed=3)])

@@ -212,6 +212,98 @@ def test_texture_corner_albedo(tmp_path):
     np.testing.assert_allclose(sc.tex_albedo[0], [0.5, 0.5, 0.5], atol=1e-7)
 
 
+def _np_sample(tex, s, t):
+    """The sampling contract restated in numpy float32: level 0, GL_LINEAR, GL_REPEAT."""
+    f = np.float32
+    h, w, ch = tex.shape
+    s, t = f(s), f(t)
+    s = s if np.isfinite(s) else f(0)
+    t = t if np.isfinite(t) else f(0)
+    s = f(s - np.floor(s))
+    t = f(t - np.floor(t))
+    x, y = f(s * f(w) - f(0.5)), f(t * f(h) - f(0.5))
+    fx, fy = np.floor(x), np.floor(y)
+    a, b = f(x - fx), f(y - fy)
+    i0, j0 = int(fx), int(fy)
+    i1, j1 = (i0 + 1) % w, (j0 + 1) % h
+    i0, j0 = i0 % w, j0 % h
+    wt = [f(f(1) - a) * f(f(1) - b), a * f(f(1) - b), f(f(1) - a) * b, a * b]
+
+    def texel(i, j, k):
+        if k >= ch or (ch == 2 and k == 2):
+            return f(0)
+        return f(f(tex[j, i, k]) / f(255))
+
+    out = np.zeros(3, np.float32)
+    for k in range(3):
+        acc = f(wt[0] * texel(i0, j0, k))
+        acc = f(acc + f(wt[1] * texel(i1, j0, k)))
+        acc = f(acc + f(wt[2] * texel(i0, j1, k)))
+        out[k] = f(acc + f(wt[3] * texel(i1, j1, k)))
+    return out
+
+
+@pytest.mark.parametrize("w,h,ch", [(1, 1, 3), (5, 4, 1), (7, 3, 2), (8, 8, 3), (3, 9, 4)])
+def test_texture_sampler_contract(w, h, ch):
+    """srt_texture_sample (csrc/scene.cpp TextureSample) against a numpy restatement of the contract, bit for bit,
+    over ordinary, wrapped, boundary and non-finite coordinates."""
+    rng = np.random.default_rng(w * 100 + h * 10 + ch)
+    tex = rng.integers(0, 256, (h, w, ch), dtype=np.uint8)
+    pts = list(rng.uniform(-3, 3, (40, 2)).astype(np.float32))
+    pts += [(0, 0), (1, 1), (-0.0, 0.5), (0.999999, 1e-9), (-1e-9, -1e-9), (1e20, -1e20), (np.nan, 0.25),
+            (np.inf, -np.inf), ((0.5 + 2) / w, (0.5 + 1) / h)]
+    for s, t in pts:
+        got = S.texture_sample(tex, s, t)
+        want = _np_sample(tex, s, t)
+        assert (got.view(np.uint32) == want.view(np.uint32)).all(), (s, t, got, want)
+    # a texel centre returns that texel exactly
+    i, j = w // 2, h // 2
+    c = S.texture_sample(tex, np.float32((i + 0.5) / w), np.float32((j + 0.5) / h))
+    exp = [tex[j, i, k] / np.float32(255) if k < ch and not (ch == 2 and k == 2) else 0 for k in range(3)]
+    np.testing.assert_array_equal(c, np.float32(exp))
+
+
+OBJ_UV = """mtllib m.mtl
+v 0 0 0
+v 1 0 0
+v 1 1 0
+v 0 1 0
+vt 0.1 0.2
+vt 0.9 0.2
+vt 0.9 0.8
+vt 0.1 0.8
+usemtl tex
+f 1/1 2/2 3/3 4/4
+f 1//1 2//1 3//1
+f 1/4/1 3/2/1 4/1/1
+"""
+
+
+def test_loader_texcoords(tmp_path):
+    """vt indices per corner (model_loader.cpp:65-71,82-143): the quad's second triangle takes vt 1, 3, 4; a face
+    without vt keeps (0,0); the default loader (has_texcoords never set, types.h:105) keeps every uv at (0,0)."""
+    _write_png(tmp_path / "t.png", 2, 2, [10, 20, 30] * 4)
+    (tmp_path / "m.mtl").write_text("newmtl tex\nKd 1 1 1\nNs 30\nmap_Kd t.png\n")
+    (tmp_path / "m.obj").write_text(OBJ_UV)
+    plain = S.Scene.from_models([S.load_obj(tmp_path / "m.obj")])
+    assert (plain.verts["uv"] == 0).all() and not plain.sample_textures
+    sc = S.Scene.from_models([S.load_obj(tmp_path / "m.obj", texcoords=True)])
+    assert sc.sample_textures and len(sc.textures) == 1 and sc.textures[0].shape == (2, 2, 3)
+    assert sc.mats[0]["use_texture"] == 1 and tuple(sc.mats[0]["handle"]) == (0, 0)
+    vt = [(0.1, 0.2), (0.9, 0.2), (0.9, 0.8), (0.1, 0.8)]
+    P = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (0, 1, 0)]
+    z = (0, 0)
+    want = [(P[0], P[1], P[2], vt[0], vt[1], vt[2]), (P[0], P[2], P[3], vt[0], vt[2], vt[3]),
+            (P[0], P[1], P[2], z, z, z), (P[0], P[2], P[3], vt[3], vt[1], vt[0])]
+    got = []
+    for tri in sc.tris:  # BVH order: compare as a multiset
+        c = list(tri["v"])
+        got.append(tuple(tuple(float(x) for x in sc.verts["pos"][i]) for i in c)
+                   + tuple(tuple(float(x) for x in sc.verts["uv"][i]) for i in c))
+    f = lambda e: tuple(tuple(float(np.float32(x)) for x in v) for v in e)  # noqa: E731
+    assert sorted(got) == sorted(f(e) for e in want)
+
+
 def test_missing_obj_raises(tmp_path):
     with pytest.raises(S.SrtError):
         S.load_obj(tmp_path / "nope.obj")
