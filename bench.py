@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--max-depth", type=int, default=5)
     ap.add_argument("--synthetic-tris", type=int, default=10_000_000)
-    ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--band-rows", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()

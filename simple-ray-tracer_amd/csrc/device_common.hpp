@@ -24,7 +24,8 @@ struct KParams {
   float4* accum;
   uint32_t* out;
   unsigned long long* stats;
-  unsigned long long* batch_ctr;  // next unclaimed 64-item batch of the launch (zeroed before it)
+  uint32_t* batch_ctr;     // next unclaimed 64-item batch of the launch (zeroed before it)
+  int tail_start;          // batches from which a claim takes one batch (LaunchSamples)
   int W, H, WH;
   int light_count;   // lightCount uniform (loop count)
   int light_records; // records in the light SSBO; index >= light_records reads zeros
@@ -48,6 +49,9 @@ struct KParams {
   const float4* tex_texels;  // RGBA32F texels of all textures
   const uint4* tex_info;     // per texture: first texel, width, height
   uint32_t n_tex;
+  const uint32_t* tile_order;  // the launch's tiles in schedule order (nullptr: natural order)
+  uint32_t* tile_cost;         // per tile: first-frame bounces recorded for the next launch's order (or nullptr)
+  unsigned long long* wave_trace;  // diagnostic build (SRT_WAVE_TRACE): 4 stamps per wave
 };
 
 // Dynamic LDS of the path-tracing kernels: [scene copy (LDS mode)] [per-lane stacks].

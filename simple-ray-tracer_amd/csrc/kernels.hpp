@@ -31,6 +31,13 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
   return __popcll(mask & ((1ull << lane) - 1ull));
 }
 
+#ifndef SRT_TILE_SCHED
+#define SRT_TILE_SCHED 1  // tiles of each frame in the last launch's cost order
+#endif
+#ifndef SRT_BOUNCE_CAP
+#define SRT_BOUNCE_CAP (1 << 20)  // bounces after which a path is cut (and counted in stack_overflow)
+#endif
+
 #ifndef SRT_GLOBAL_WAVES
 #define SRT_GLOBAL_WAVES 4
 #endif
@@ -40,6 +47,10 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
 template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX>
 __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_kernel(KParams kp) {
   const int tid = threadIdx.x;
+#ifdef SRT_WAVE_TRACE
+  const unsigned long long tw0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long tw2 = 0;
+#endif
   if constexpr (LDSM) {  // the block copies the scene (nodes + triangles) into LDS once
     const int total = kp.nodes_f4 + kp.tris_f4;
     for (int i = tid; i < total; i += blockDim.x)
@@ -47,6 +58,9 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
     __syncthreads();
   }
   const int lane = tid & 63;
+#ifdef SRT_WAVE_TRACE
+  const unsigned long long tw1 = __builtin_amdgcn_s_memrealtime();
+#endif
   Lane ln;
   if constexpr (LDSM) {
     ln.stk = reinterpret_cast<uint32_t*>(g_smem + kp.stack_base_f4) + tid;
@@ -65,17 +79,23 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
   const int tiles_x = (kp.W + 7) >> 3;
   const int n_tiles = tiles_x * ((kp.local_rows + 7) >> 3);
   const int n_batches = n_tiles * kp.nframes;  // < 2^31: the host bounds the frames per launch
-  // batches are claimed one at a time from a launch-wide counter, so waves
-  // that drew cheap tiles take more of them (no static-share tail).  The
-  // next batch is claimed one ahead: lane 0's atomic returns while the
-  // current batch is consumed, and is only read (broadcast) when needed.
-  // kClaim consecutive batches per claim.
-  // `batch` and everything derived from it are wave-uniform (scalar registers).
-  unsigned long long claimed = 0;
-  if (lane == 0) claimed = atomicAdd(kp.batch_ctr, 1ull);
-  int batch = __builtin_amdgcn_readfirstlane((int)__shfl(claimed, 0)) * kClaim;
-  int claim_left = kClaim - 1;  // batches of the current claim after `batch`
-  if (lane == 0) claimed = atomicAdd(kp.batch_ctr, 1ull);
+  // batches are claimed from a launch-wide counter of batches, so waves that
+  // drew cheap tiles take more of them (no static-share tail).  A claim takes
+  // kClaim consecutive batches and the next claim is issued one ahead (lane
+  // 0's atomic returns while the current batch is consumed, and is only read,
+  // broadcast, when needed).  From kp.tail_start on (16 claims per wave
+  // before the end, pathtrace.hip) a claim takes one batch: a wave then holds
+  // at most two batches, so the launch's tail is not set by slow waves still
+  // draining several expensive batches each (tools/wave_trace.py).
+  // `batch` and everything derived from it are wave-uniform (scalar
+  // registers); the counter's overshoot past n_batches stays below 2^31.
+  uint32_t claimed = 0;
+  int claim_sz = kp.tail_start > 0 ? kClaim : 1;  // size of the claim in flight
+  if (lane == 0) claimed = atomicAdd(kp.batch_ctr, (uint32_t)claim_sz);
+  int batch = __builtin_amdgcn_readfirstlane((int)__shfl(claimed, 0));
+  int claim_left = claim_sz - 1;  // batches of the current claim after `batch`
+  claim_sz = batch < kp.tail_start ? kClaim : 1;
+  if (lane == 0) claimed = atomicAdd(kp.batch_ctr, (uint32_t)claim_sz);
   int batch_next = 0;         // items of `batch` already handed out
 
   // per-lane sample / path / traversal state
@@ -111,6 +131,10 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
     }
   };
   auto finish_sample = [&]() {
+    if (SRT_TILE_SCHED && kp.tile_cost && fidx == 0) {  // this tile's cost for the next launch's order: its first frame's bounces
+      const int ly = li / kp.W, px = li - ly * kp.W;
+      atomicAdd(&kp.tile_cost[(ly >> 3) * tiles_x + (px >> 3)], (uint32_t)(bounces + 1));
+    }
     color = color + T * mk(0.05f, 0.05f, 0.05f);  // skyColor, raytrace_compute.glsl:219,292
     kp.lbuf[(size_t)fidx * (size_t)kp.local_pixels + (size_t)li] = make_float4(color.x, color.y, color.z, 0.0f);
     has_work = false;
@@ -125,12 +149,23 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
     // ---- (A) idle lanes take the next items of the wave's batches ----
     for (;;) {
       const unsigned long long idle = __ballot(!has_work);
+#ifdef SRT_WAVE_TRACE
+      if (batch >= n_batches && tw2 == 0) tw2 = __builtin_amdgcn_s_memrealtime();
+#endif
       if (idle == 0ull || batch >= n_batches) break;
       const int avail = 64 - batch_next;
       const int r = lane_rank(idle, lane);
-      // the batch's frame and 8x8 tile (wave-uniform integer divisions, once per batch)
+      // the batch's frame and 8x8 tile (wave-uniform integer divisions, once per
+      // batch): frame by frame, and within a frame the tiles in tile_order (the
+      // last launch's tiles by decreasing cost, order_tiles_kernel), read by a
+      // scalar load (constant address space: the order is read-only here)
       const int frame_i = batch / n_tiles;
-      const int tile = batch - frame_i * n_tiles;
+      const int trank = batch - frame_i * n_tiles;
+#if SRT_TILE_SCHED
+      const int tile = (int)((const __attribute__((address_space(4))) uint32_t*)(kp.tile_order))[trank];
+#else
+      const int tile = trank;
+#endif
       const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
       const int samp = (kp.frame_first + frame_i) % kp.WH;
       // row band of the tile when bands are whole tiles (the default 8 rows)
@@ -179,9 +214,10 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
           ++batch;
           --claim_left;
         } else {
-          batch = __builtin_amdgcn_readfirstlane((int)__shfl(claimed, 0)) * kClaim;
-          claim_left = kClaim - 1;
-          if (lane == 0) claimed = atomicAdd(kp.batch_ctr, 1ull);
+          batch = __builtin_amdgcn_readfirstlane((int)__shfl(claimed, 0));
+          claim_left = claim_sz - 1;
+          claim_sz = batch < kp.tail_start ? kClaim : 1;
+          if (lane == 0) claimed = atomicAdd(kp.batch_ctr, (uint32_t)claim_sz);
         }
         batch_next = 0;
       }
@@ -369,7 +405,7 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
         // The reference's loop has no depth cap (Russian roulette clamps the
         // survival probability to >= 0.1).  A path still alive after 2^20
         // bounces is cut (and counted) so a pathological scene cannot hang the GPU.
-        if (++bounces >= (1 << 20) && !term) {
+        if (++bounces >= SRT_BOUNCE_CAP && !term) {
           term = true;
           bump<COUNT>(c, ST_OVERFLOW);
         }
@@ -410,7 +446,51 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
     atomicAdd(&kp.stats[ST_DBG_SHADE], d_shade);
   }
 #endif
+#ifdef SRT_WAVE_TRACE
+  if (lane == 0 && kp.wave_trace) {
+    unsigned long long* w = kp.wave_trace + 4 * ((size_t)blockIdx.x * (blockDim.x >> 6) + (tid >> 6));
+    w[0] = tw0;
+    w[1] = tw1;
+    w[2] = tw2;
+    w[3] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   flush_counters<COUNT>(kp, c);
+}
+
+// Schedule of the next sample_kernel launch: its n tiles by decreasing cost
+// (the first-frame bounce counts the last launch recorded, bucketed on a
+// quarter-octave log scale), so the launch's tail runs the cheapest tiles.
+// Resets the costs for the next recording.  One block.  The order only
+// decides which wave traces which samples, never a sample's value.
+__device__ __forceinline__ int cost_bucket(uint32_t c) {
+  const int b = (int)(__log2f((float)c + 1.0f) * 4.0f);
+  return b < 63 ? b : 63;
+}
+__global__ __launch_bounds__(1024) void order_tiles_kernel(uint32_t* cost, uint32_t* order, int n) {
+  __shared__ uint32_t hist[64];
+  if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[cost_bucket(cost[i])], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // exclusive offsets, most expensive bucket first
+    uint32_t s = 0;
+    for (int b = 63; b >= 0; --b) {
+      const uint32_t h = hist[b];
+      hist[b] = s;
+      s += h;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    order[atomicAdd(&hist[cost_bucket(cost[i])], 1u)] = (uint32_t)i;
+    cost[i] = 0u;
+  }
+}
+
+__global__ __launch_bounds__(256) void iota_kernel(uint32_t* order, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) order[i] = (uint32_t)i;
 }
 
 // Ordered sum of the sample buffer into the accumulation image (raytrace_compute.glsl:

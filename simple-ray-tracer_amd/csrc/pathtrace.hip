@@ -111,10 +111,17 @@ struct srt_context {
   float4* d_lbuf = nullptr;
   uint32_t* d_gstack = nullptr;  // global-scene mode traversal stacks
   size_t gstack_bytes = 0;
+  // tile schedule: per-tile costs recorded by the last launch and the next
+  // launch's order (order_tiles_kernel); costs_for = the tile count they describe
+  uint32_t* d_tile_cost = nullptr;
+  uint32_t* d_tile_order = nullptr;
+  int tile_cap = 0, tile_costs_for = -1;
+  bool tile_schedule = true;  // SRT_TILE_ORDER=0: natural tile order
   unsigned long long* d_batch_ctr = nullptr;  // one batch counter per chunk launch
   int batch_ctr_cap = 0;
   size_t lbuf_bytes = 0;
   size_t lbuf_cap = (size_t)16 << 30;  // SRT_SAMPLE_BUFFER_MB
+  int tail_claims = 16;  // SRT_TAIL_CLAIMS: claims per wave before the end from which claims take one batch
   int trav_frac16 = 8;                 // SRT_TRAV_FRAC16 (measured best on Rubik 1080p with 2-triangle leaf steps)
   int num_cus = 256;
   // stats
@@ -122,6 +129,17 @@ struct srt_context {
   srt_stats stats{};
   // per-chunk HIP events around the sample kernel of the last render call
   std::vector<hipEvent_t> ev;
+  struct Occupancy {
+    const void* fn;
+    size_t lds;
+    int per_cu;
+  };
+  std::vector<Occupancy> occupancy;  // resident blocks per CU of each sample_kernel instance
+#ifdef SRT_WAVE_TRACE
+  unsigned long long* d_trace = nullptr;
+  size_t trace_bytes = 0;
+  int trace_waves = 0;
+#endif
   int ev_used = 0;
 };
 
@@ -283,10 +301,18 @@ constexpr size_t kLdsBytes = 160 * 1024;
 
 template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX>
 int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
+  // resident blocks per CU, queried once per (kernel instance, LDS size): the
+  // query runs on the host between the launch's timing events otherwise
+  const void* fn = reinterpret_cast<const void*>(&srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX>);
   int per_cu = 0;
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX>, BLOCK,
-                                                        lds));
-  per_cu = std::max(per_cu, 1);
+  for (const auto& e : c->occupancy)
+    if (e.fn == fn && e.lds == lds) per_cu = e.per_cu;
+  if (per_cu == 0) {
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX>,
+                                                          BLOCK, lds));
+    per_cu = std::max(per_cu, 1);
+    c->occupancy.push_back({fn, lds, per_cu});
+  }
   const int blocks = c->num_cus * per_cu;
   if constexpr (!LDSM) {  // global-scene mode: every lane's full stack in HBM (backing the LDS ring)
     const size_t lanes = (size_t)blocks * BLOCK;
@@ -301,8 +327,28 @@ int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
     kp.gstack = c->d_gstack;
     kp.gstack_stride = (int)lanes;
   }
+#ifdef SRT_WAVE_TRACE
+  {  // diagnostic build: 4 realtime stamps per wave of the last launch
+    const size_t need = (size_t)blocks * (BLOCK / 64) * 4 * sizeof(unsigned long long);
+    if (need > c->trace_bytes) {
+      FreeDev(c->d_trace);
+      HIP_OK(hipMalloc(&c->d_trace, need));
+      c->trace_bytes = need;
+    }
+    c->trace_waves = blocks * (BLOCK / 64);
+    kp.wave_trace = c->d_trace;
+  }
+#endif
+  {  // single-batch claims for the last tail_claims * kClaim batches per wave (sample_kernel; measured
+     // with tools/tail_sweep.sh: 2 -> 16 halves the launch's tail)
+    const long long waves = (long long)blocks * (BLOCK / 64);
+    const long long n_batches = (long long)((kp.W + 7) >> 3) * ((kp.local_rows + 7) >> 3) * kp.nframes;
+    kp.tail_start = (int)std::max<long long>(0, n_batches - (long long)c->tail_claims * srt::kClaim * waves);
+  }
+  HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
   hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX>), dim3(blocks), dim3(BLOCK), lds, c->stream, kp);
   HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
   return SRT_OK;
 }
 
@@ -348,7 +394,8 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   const size_t per_frame = (size_t)npx * sizeof(float4);
   // frames per launch: what the sample buffer holds, and n_tiles * frames < 2^31 (the kernel's batch index)
   const size_t n_tiles = (size_t)((kp.W + 7) >> 3) * (size_t)((kp.local_rows + 7) >> 3);
-  const size_t max_frames = std::max<size_t>(1, (size_t)0x7FFFFFFF / std::max<size_t>(1, n_tiles) - 1);
+  // (less 2^20: the batch counter overshoots the end by up to (kClaim + 1) claims per wave)
+  const size_t max_frames = std::max<size_t>(1, ((size_t)0x7FFFFFFF - ((size_t)1 << 20)) / std::max<size_t>(1, n_tiles));
   const int chunk = (int)std::max<size_t>(
       1, std::min<size_t>(std::min<size_t>((size_t)kp.nframes, max_frames), c->lbuf_cap / per_frame));
   const size_t need = per_frame * (size_t)chunk;
@@ -383,16 +430,38 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
     kc.frame_first = kp.frame_first + f0;
     kc.nframes = std::min(chunk, kp.nframes - f0);
     kc.write_output = (f0 + chunk >= kp.nframes) ? kp.write_output : 0;
-    kc.batch_ctr = c->d_batch_ctr + f0 / chunk;
+    kc.batch_ctr = reinterpret_cast<uint32_t*>(c->d_batch_ctr + f0 / chunk);
+    {  // tile order: the tiles the last launch found most expensive first (SRT_TILE_ORDER=0: natural order)
+      const int nt = (int)n_tiles;
+      if (nt > c->tile_cap) {
+        FreeDev(c->d_tile_cost);
+        FreeDev(c->d_tile_order);
+        c->d_tile_cost = c->d_tile_order = nullptr;
+        c->tile_cap = 0;
+        HIP_OK(hipMalloc(&c->d_tile_cost, sizeof(uint32_t) * (size_t)nt));
+        HIP_OK(hipMalloc(&c->d_tile_order, sizeof(uint32_t) * (size_t)nt));
+        c->tile_cap = nt;
+        c->tile_costs_for = -1;
+      }
+      if (c->tile_schedule && c->tile_costs_for == nt) {
+        hipLaunchKernelGGL(srt::order_tiles_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_tile_cost, c->d_tile_order,
+                           nt);
+      } else {
+        hipLaunchKernelGGL(srt::iota_kernel, dim3((nt + 255) / 256), dim3(256), 0, c->stream, c->d_tile_order, nt);
+        if (c->tile_schedule) HIP_OK(hipMemsetAsync(c->d_tile_cost, 0, sizeof(uint32_t) * (size_t)nt, c->stream));
+      }
+      HIP_OK(hipGetLastError());
+      kc.tile_order = c->d_tile_order;
+      kc.tile_cost = c->tile_schedule ? c->d_tile_cost : nullptr;
+      c->tile_costs_for = c->tile_schedule ? nt : -1;
+    }
     int rc;
-    HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
     // LDS mode: packed entries (lds_ok); global-scene mode: packed when indices fit 24 bits
     const bool pack = c->lds_ok;
     rc = c->sample_textures ? LaunchMode<true>(c, kc, lds, count, ldsm, pack)
                             : LaunchMode<false>(c, kc, lds, count, ldsm, pack);
     if (rc) return rc;
-    HIP_OK(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
-    c->ev_used += 2;
+    c->ev_used += 2;  // LaunchSamples recorded the pair around the launch
     hipLaunchKernelGGL(srt::accumulate_kernel, pgrid, dim3(256), 0, c->stream, kc, out_frames);
     HIP_OK(hipGetLastError());
   }
@@ -474,6 +543,8 @@ int srt_create(int device, void* stream, srt_context** out) {
   if (const char* e = std::getenv("SRT_FORCE_GLOBAL_SCENE")) c->force_global = e[0] == '1';
   if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_MB")) c->lbuf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
   if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_KB")) c->lbuf_cap = (size_t)std::max(1L, std::atol(e)) << 10;
+  if (const char* e = std::getenv("SRT_TAIL_CLAIMS")) c->tail_claims = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("SRT_TILE_ORDER")) c->tile_schedule = e[0] != '0';
   if (const char* e = std::getenv("SRT_TRAV_FRAC16")) c->trav_frac16 = std::max(0, std::min(16, std::atoi(e)));
   {
     hipDeviceProp_t prop;
@@ -508,7 +579,7 @@ int srt_destroy(srt_context* c) {
   FreeDev(c->d_nodes); FreeDev(c->d_tris); FreeDev(c->d_mats); FreeDev(c->d_bvhs); FreeDev(c->d_lights);
   FreeDev(c->d_tex); FreeDev(c->d_tex_info); FreeDev(c->d_tri_uv);
   FreeDev(c->d_noise_xy); FreeDev(c->d_noise_u); FreeDev(c->d_stats); FreeDev(c->d_lbuf); FreeDev(c->d_gstack);
-  FreeDev(c->d_batch_ctr);
+  FreeDev(c->d_batch_ctr); FreeDev(c->d_tile_cost); FreeDev(c->d_tile_order);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (!c->images_external) { FreeDev(c->d_accum); FreeDev(c->d_out); }
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -630,6 +701,19 @@ extern "C" int srt_debug_phase_cycles(srt_context* c, unsigned long long out[58]
   HIP_OK(hipStreamSynchronize(c->stream));
   return SRT_OK;
 }
+
+#ifdef SRT_WAVE_TRACE
+// Diagnostic build: copies the last launch's per-wave stamps (start, scene in
+// LDS, batches exhausted, end; s_memrealtime ticks) into out[4 * n], n <= waves.
+extern "C" int srt_debug_wave_trace(srt_context* c, unsigned long long* out, int n) {
+  if (!c || !out || !c->d_trace) return -1;
+  n = std::min(n, c->trace_waves);
+  HIP_OK(hipMemcpyAsync(out, c->d_trace, (size_t)n * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                        c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  return n;
+}
+#endif
 
 int srt_last_kernel_ms(srt_context* c, float* ms) {
   if (!c || !ms) return SRT_ERR_INVALID;

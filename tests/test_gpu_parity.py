@@ -205,6 +205,28 @@ def test_sample_buffer_chunking_invariance(rubik, monkeypatch):
     assert bits_equal(a, b).all() and (o == p).all()
 
 
+def test_schedule_invariance(rubik, monkeypatch):
+    """The work schedule decides which wave traces which sample, never a value: the tile order learned
+    from the previous launch, the natural order, and single-batch claims everywhere or nowhere give the
+    same bits."""
+    setup = R.make_setup(72, 56, show_model=True, models=[rubik])
+    r = R.Renderer(setup)
+    try:
+        r.render(4, count=True)  # records the tile costs
+        r.render(4)              # runs in the learned order
+        r.finish()
+        a, o = r.accum(), r.output()
+    finally:
+        r.close()
+    for env in ({"SRT_TILE_ORDER": "0"}, {"SRT_TAIL_CLAIMS": "0"}, {"SRT_TAIL_CLAIMS": "100000"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        b, p, _ = gpu_render(setup, 4)
+        assert bits_equal(a, b).all() and (o == p).all(), env
+        for k in env:
+            monkeypatch.delenv(k)
+
+
 @pytest.mark.parametrize("nranks,band", [(2, 16), (3, 8)])
 def test_row_band_tiling_reassembles(rubik, nranks, band):
     import torch
