@@ -64,7 +64,7 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
   Lane ln;
   if constexpr (LDSM) {
     ln.stk = reinterpret_cast<uint32_t*>(g_smem + kp.stack_base_f4) + tid;
-    ln.stride = blockDim.x;
+    ln.stride = BLOCK;  // a compile-time stride: stack addressing by shifts, no v_mul_lo_u32
   } else {  // the top kShortStack entries in an LDS ring, the rest in HBM (lane-interleaved, coalesced)
     ln.stk = reinterpret_cast<uint32_t*>(g_smem) + tid;
     ln.stride = BLOCK;
