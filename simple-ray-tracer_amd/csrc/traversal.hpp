@@ -390,28 +390,37 @@ __device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln,
 }
 
 // Nothing current: pop one entry (visited if it still beats the running
-// distance), or finish this BVH.  A lane whose next BVH is pending (`start`,
-// set up at the next iteration) does nothing.
+// distance).  A lane whose stack is empty waits for trav_finish at the end of
+// the iteration (its later sub-steps have nothing to do either), so the pop
+// is one branch.  A lane whose next BVH is pending (`start`, set up at the
+// next iteration) does nothing.
 template <bool LDSM, bool PACK>
-__device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav& t, bool any) {
-  if (t.active & !t.start & (t.cnt == 0) & (t.ref == kNoneRef)) {
-    if (t.sp > 0) {
-      --t.sp;
-      uint32_t r, n;
-      float et;
-      if constexpr (LDSM) {
-        slot_read<true>(ln.stk, ln.stride, t.sp, r, n, et);
-      } else if (t.sp < t.lo) {  // below the LDS ring: from HBM (rare)
-        slot_read<PACK>(ln.gstk, ln.gstride, t.sp, r, n, et);
-        t.lo = t.sp;
-      } else {
-        slot_read<PACK>(ln.stk, ln.stride, t.sp & (kShortStack - 1), r, n, et);
-      }
-      const bool take = et < t.dist;
-      t.ref = take ? r : kNoneRef;
-      t.cnt = take ? n : 0u;
-    } else if ((any && t.hit != kNoneRef) || t.bi + 1 >= kp.bvh_count) {
-      t.active = false;  // CheckHit's loop over bvh_count is complete
+__device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav& t) {
+  if (t.active & !t.start & (t.cnt == 0) & (t.ref == kNoneRef) & (t.sp > 0)) {
+    --t.sp;
+    uint32_t r, n;
+    float et;
+    if constexpr (LDSM) {
+      slot_read<true>(ln.stk, ln.stride, t.sp, r, n, et);
+    } else if (t.sp < t.lo) {  // below the LDS ring: from HBM (rare)
+      slot_read<PACK>(ln.gstk, ln.gstride, t.sp, r, n, et);
+      t.lo = t.sp;
+    } else {
+      slot_read<PACK>(ln.stk, ln.stride, t.sp & (kShortStack - 1), r, n, et);
+    }
+    const bool take = et < t.dist;
+    t.ref = take ? r : kNoneRef;
+    t.cnt = take ? n : 0u;
+  }
+}
+
+// End of an iteration: a lane with nothing current and an empty stack has
+// finished this BVH -- CheckHit's loop over bvh_count is complete (or, for a
+// shadow ray, a hit was found), or the next BVH is set up next iteration.
+__device__ __forceinline__ void trav_finish(const KParams& kp, Trav& t, bool any) {
+  if (t.active & !t.start & (t.cnt == 0) & (t.ref == kNoneRef) & (t.sp == 0)) {
+    if ((any && t.hit != kNoneRef) || t.bi + 1 >= kp.bvh_count) {
+      t.active = false;
     } else {
       ++t.bi;
       t.start = true;
@@ -430,7 +439,7 @@ __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln,
       if (t.cnt > 0) trav_leaf<COUNT, LDSM>(kp, c, t, any);
     }
     DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K + 2, t.active & !t.start & (t.cnt == 0) & (t.ref == kNoneRef));
-    trav_pop<LDSM, PACK>(kp, ln, t, any);
+    trav_pop<LDSM, PACK>(kp, ln, t);
     trav_substeps<COUNT, LDSM, PACK, K + 1>(kp, ln, c, t, any);
   }
 }
@@ -445,6 +454,7 @@ __device__ __forceinline__ void trav_step(const KParams& kp, const Lane& ln, Cou
                                           bool any) {
   if (t.start) trav_begin_bvh<COUNT, LDSM>(kp, c, t, ro, rd);  // only for BVHs after the first
   trav_substeps<COUNT, LDSM, PACK, 0>(kp, ln, c, t, any);
+  trav_finish(kp, t, any);
 }
 
 }  // namespace srt
