@@ -147,8 +147,15 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
   for (;;) {
     PHASE_STAMP(t_a);
     // ---- (A) idle lanes take the next items of the wave's batches ----
+    // First every idle lane is assigned an item (a pass per batch the idle
+    // lanes span: scalar batch decomposition, a few vector ops), then the
+    // assigned lanes start their samples in one pass, so a refill that spans
+    // two batches issues the camera-ray setup (and waits for its noise
+    // fetch) once.
+    bool fresh = false;          // assigned an item in this refill
+    int a_pl = 0, a_gy = 0, a_f = 0, a_samp = 0;  // its pixel (x | local row << 16), global row, frame, sample index
     for (;;) {
-      const unsigned long long idle = __ballot(!has_work);
+      const unsigned long long idle = __ballot(!has_work & !fresh);
 #ifdef SRT_WAVE_TRACE
       if (batch >= n_batches && tw2 == 0) tw2 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -170,7 +177,7 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
       const int samp = (kp.frame_first + frame_i) % kp.WH;
       // row band of the tile when bands are whole tiles (the default 8 rows)
       const int band_u = (kp.band_rows & 7) == 0 ? ty / (kp.band_rows >> 3) : -1;
-      if (!has_work && r < avail) {
+      if (!has_work & !fresh & (r < avail)) {
         const int item = batch_next + r;
         const int px = tx * 8 + (item & 7), ly = ty * 8 + (item >> 3);
         if (px < kp.ext_w && ly < kp.local_rows) {
@@ -178,32 +185,12 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
           if (band_u >= 0) band = band_u;
           else band = ly / kp.band_rows;
           const int yy = (band * kp.nranks + kp.rank) * kp.band_rows + (ly - band * kp.band_rows);
-          if (yy < kp.ext_h) {
-            has_work = true;
-            x = px;
-            gy = yy;
-            li = ly * kp.W + px;
-            fidx = frame_i;
-            ln.base = gy * kp.H + x;
-            // GetRay (raytrace_compute.glsl:78-90) with SampleSquare (raytrace_utils.glsl:10-17)
-            const float2 nz = kp.noise_xy[wrap_index(ln.base + samp, kp.WH)];
-            bump<COUNT>(c, ST_RNGSQ);
-            bump<COUNT>(c, ST_SAMPLES);
-            const f3 p00 = mk(kp.p00x, kp.p00y, kp.p00z);
-            const f3 du = mk(kp.dux, kp.duy, kp.duz);
-            const f3 dv = mk(kp.dvx, kp.dvy, kp.dvz);
-            const f3 ps = (p00 + du * ((float)x + (nz.x - 0.5f))) + dv * ((float)gy + (nz.y - 0.5f));
-            ro = center;
-            rd = ps - center;
-            tmax = __builtin_inff();
-            T = mk(1.0f, 1.0f, 1.0f);
-            color = mk(0.0f, 0.0f, 0.0f);
-            depth = kp.max_depth;
-            randIndex = 0;
-            bounces = 0;
-            shadow_phase = false;
-            term = false;
-            start_ray();
+          if (yy < kp.ext_h) {  // else the item is outside the dispatch extent: the lane tries the next one
+            fresh = true;
+            a_pl = px | (ly << 16);
+            a_gy = yy;
+            a_f = frame_i;
+            a_samp = samp;
           }
         }
       }
@@ -221,6 +208,33 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
         }
         batch_next = 0;
       }
+    }
+    if (fresh) {
+      has_work = true;
+      x = a_pl & 0xFFFF;
+      gy = a_gy;
+      li = (a_pl >> 16) * kp.W + x;
+      fidx = a_f;
+      ln.base = gy * kp.H + x;
+      // GetRay (raytrace_compute.glsl:78-90) with SampleSquare (raytrace_utils.glsl:10-17)
+      const float2 nz = kp.noise_xy[wrap_index(ln.base + a_samp, kp.WH)];
+      bump<COUNT>(c, ST_RNGSQ);
+      bump<COUNT>(c, ST_SAMPLES);
+      const f3 p00 = mk(kp.p00x, kp.p00y, kp.p00z);
+      const f3 du = mk(kp.dux, kp.duy, kp.duz);
+      const f3 dv = mk(kp.dvx, kp.dvy, kp.dvz);
+      const f3 ps = (p00 + du * ((float)x + (nz.x - 0.5f))) + dv * ((float)gy + (nz.y - 0.5f));
+      ro = center;
+      rd = ps - center;
+      tmax = __builtin_inff();
+      T = mk(1.0f, 1.0f, 1.0f);
+      color = mk(0.0f, 0.0f, 0.0f);
+      depth = kp.max_depth;
+      randIndex = 0;
+      bounces = 0;
+      shadow_phase = false;
+      term = false;
+      start_ray();
     }
     if (__ballot(has_work) == 0ull) break;
     PHASE_STAMP(t_b);
