@@ -104,7 +104,7 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
   f3 ro = mk(0.f, 0.f, 0.f), rd = mk(0.f, 0.f, 1.f), T, color, q0, q1, nd;
   float tmax = 0.0f;
   int depth = 0, randIndex = 0, hit_sphere = -1, bounces = 0;
-  bool shadow_phase = false, term = false;
+  bool shadow_phase = false, term = false, pending = false;
   Trav tr;
   tr.active = false;
   tr.start = false;
@@ -234,6 +234,12 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
       bounces = 0;
       shadow_phase = false;
       term = false;
+      pending = true;
+    }
+    // every lane with a ray to start (new samples, and the shadow / bounce
+    // rays the last shading phase set up) starts it here, in one pass
+    if (pending) {
+      pending = false;
       start_ray();
     }
     if (__ballot(has_work) == 0ull) break;
@@ -275,7 +281,7 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
           rd = nd;  // the bounce ray starts at the same hit point as the shadow ray
           tmax = __builtin_inff();
           shadow_phase = false;
-          start_ray();
+          pending = true;  // started with the refill's new rays (one start_ray pass)
         }
       } else if (!hit) {
         finish_sample();
@@ -428,13 +434,13 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
           rd = sdir;
           tmax = smax;
           shadow_phase = true;
-          start_ray();
+          pending = true;  // started with the refill's new rays (one start_ray pass)
         } else if (term) {
           finish_sample();
         } else {
           rd = nd;
           tmax = __builtin_inff();
-          start_ray();
+          pending = true;  // started with the refill's new rays (one start_ray pass)
         }
       }
     }
