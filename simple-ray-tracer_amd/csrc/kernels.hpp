@@ -349,11 +349,23 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
           const float inten = L.intensity * fo;
           const float lpdf = luminance(mk(inten, inten, inten));
           const float ris = lpdf * (float)n;
-          float total = 0.0f, pdf = 0.0f;
-          for (int i = 0; i < n; ++i) {
+          // Iteration i selects when its draw r < ris / total_i with total_i =
+          // (i + 1) * ris.  When ris / total is NaN (ris is 0 -- the zero record
+          // past the lights -- or not finite) it is NaN at every i: no draw can
+          // select and the draws are skipped: they never change a value (the
+          // counters count the fetches the kernel makes).  This ~1-in-2n case
+          // otherwise costs n - 1 dependent gathers, and with ~35 shading lanes
+          // nearly every wave has such a lane.
+          float total = ris, pdf = 0.0f;  // 0 + ris
+          if (u_sel0 < (ris / total)) {
+            pdf = lpdf;
+            selected = true;
+          }
+          const bool draws = !selected && (ris / total == ris / total);
+          for (int i = 1; i < n; ++i) {
             total += ris;
-            if (!selected) {
-              const float r = (i == 0) ? u_sel0 : randU<COUNT>(kp, ln, c, p.y + (float)i, p.z + (float)i);
+            if (draws && !selected) {
+              const float r = randU<COUNT>(kp, ln, c, p.y + (float)i, p.z + (float)i);
               if (r < (ris / total)) {
                 pdf = lpdf;
                 selected = true;
