@@ -49,6 +49,9 @@ struct KParams {
   const float4* tex_texels;  // RGBA32F texels of all textures
   const uint4* tex_info;     // per texture: first texel, width, height
   uint32_t n_tex;
+  // LDS copies of the light and material records (read per shading), when they fit
+  int lights_lds, lights_base_f4;  // light_records + 1 records of 2 float4
+  int mats_lds, mats_base_f4, mat_records;  // mat_records records of 2 float4
   const uint32_t* tile_order;  // the launch's tiles in schedule order (nullptr: natural order)
   uint32_t* tile_cost;         // per tile: first-frame bounces recorded for the next launch's order (or nullptr)
   unsigned long long* wave_trace;  // diagnostic build (SRT_WAVE_TRACE): 4 stamps per wave

@@ -55,8 +55,13 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
     const int total = kp.nodes_f4 + kp.tris_f4;
     for (int i = tid; i < total; i += blockDim.x)
       g_smem[i] = (i < kp.nodes_f4) ? kp.nodes[i] : kp.tris[i - kp.nodes_f4];
-    __syncthreads();
   }
+  {  // and the light and material records, when they fit (shading reads them from LDS)
+    const int nl = kp.lights_lds ? 2 * (kp.light_records + 1) : 0, nm = kp.mats_lds ? 2 * kp.mat_records : 0;
+    for (int i = tid; i < nl; i += blockDim.x) g_smem[kp.lights_base_f4 + i] = kp.lights[i];
+    for (int i = tid; i < nm; i += blockDim.x) g_smem[kp.mats_base_f4 + i] = kp.mats[i];
+  }
+  __syncthreads();
   const int lane = tid & 63;
 #ifdef SRT_WAVE_TRACE
   const unsigned long long tw1 = __builtin_amdgcn_s_memrealtime();
@@ -295,7 +300,14 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
           const float4 A = tri4<LDSM>(kp, 3 * ht), B = tri4<LDSM>(kp, 3 * ht + 1), C = tri4<LDSM>(kp, 3 * ht + 2);
           rec.normal = normalize(cross(mk(A.w, B.x, B.y), mk(B.z, B.w, C.x)));
           const uint32_t mi = __float_as_uint(C.y);
-          const float4 m0 = kp.mats[2 * mi], m1 = kp.mats[2 * mi + 1];
+          float4 m0, m1;
+          if (kp.mats_lds) {
+            m0 = lds4((uint32_t)(kp.mats_base_f4 + 2 * mi) << 4);
+            m1 = lds4((uint32_t)(kp.mats_base_f4 + 2 * mi + 1) << 4);
+          } else {
+            m0 = kp.mats[2 * mi];
+            m1 = kp.mats[2 * mi + 1];
+          }
           bump<COUNT>(c, ST_MATS);
           rec.mat.albedo = mk(m0.x, m0.y, m0.z);
           if constexpr (TEX) {  // the instance for scenes whose materials sample a texture

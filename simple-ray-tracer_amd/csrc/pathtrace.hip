@@ -390,6 +390,22 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
     kp.stack_base_f4 = 0;
     lds = (size_t)block * (c->lds_ok ? 2 : 3) * sizeof(uint32_t) * (size_t)srt::kShortStack;
   }
+  {  // light and material records in LDS behind the rest, when they fit (shading reads them there)
+    lds = (lds + 15) & ~(size_t)15;
+    const size_t light_bytes = 2 * sizeof(float4) * ((size_t)kp.light_records + 1);
+    kp.lights_lds = (light_bytes <= 8192 && lds + light_bytes <= kLdsBytes) ? 1 : 0;
+    if (kp.lights_lds) {
+      kp.lights_base_f4 = (int)(lds / sizeof(float4));
+      lds += light_bytes;
+    }
+    kp.mat_records = (int)c->n_mats + 1;
+    const size_t mat_bytes = 2 * sizeof(float4) * (size_t)kp.mat_records;
+    kp.mats_lds = (kp.show_model && c->d_mats && mat_bytes <= 16384 && lds + mat_bytes <= kLdsBytes) ? 1 : 0;
+    if (kp.mats_lds) {
+      kp.mats_base_f4 = (int)(lds / sizeof(float4));
+      lds += mat_bytes;
+    }
+  }
   // sample buffer: as many frames per chunk as the buffer cap allows
   const size_t per_frame = (size_t)npx * sizeof(float4);
   // frames per launch: what the sample buffer holds, and n_tiles * frames < 2^31 (the kernel's batch index)

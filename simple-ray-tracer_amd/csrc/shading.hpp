@@ -105,7 +105,14 @@ template <bool COUNT>
 __device__ __forceinline__ LightRec load_light(const KParams& kp, Counters& c, int idx) {
   bump<COUNT>(c, ST_LIGHTS);
   const int i = (idx >= 0 && idx < kp.light_records) ? idx : kp.light_records;  // zero record
-  const float4 a = kp.lights[2 * i], b = kp.lights[2 * i + 1];
+  float4 a, b;
+  if (kp.lights_lds) {
+    a = lds4((uint32_t)(kp.lights_base_f4 + 2 * i) << 4);
+    b = lds4((uint32_t)(kp.lights_base_f4 + 2 * i + 1) << 4);
+  } else {
+    a = kp.lights[2 * i];
+    b = kp.lights[2 * i + 1];
+  }
   return LightRec{mk(a.x, a.y, a.z), a.w, mk(b.x, b.y, b.z)};
 }
 
