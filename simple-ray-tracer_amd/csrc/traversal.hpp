@@ -26,6 +26,22 @@ __device__ __forceinline__ float box_t(f3 o, f3 inv, float4 lo, float4 hi) {
 
 __device__ __forceinline__ bool box_ok(float b, float dist) { return b < dist && !isinf_f(b); }
 
+// box_ok(box_t(...), dist) with one compare fewer: `b` receives the entry
+// distance IntersectsBox returns whenever the result is true.  Equivalence:
+// for tn <= tf, b = sel and `sel < dist` already rejects sel = +inf, so only
+// -inf needs its own test; otherwise (tn > tf, or a NaN bound) IntersectsBox
+// returns +inf, which no `< dist` accepts.
+__device__ __forceinline__ bool box_test(f3 o, f3 inv, float4 lo, float4 hi, float dist, float& b) {
+  const float t0x = (lo.x - o.x) * inv.x, t0y = (lo.y - o.y) * inv.y, t0z = (lo.z - o.z) * inv.z;
+  const float t1x = (hi.x - o.x) * inv.x, t1y = (hi.y - o.y) * inv.y, t1z = (hi.z - o.z) * inv.z;
+  const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t0x, t1x), __builtin_fminf(t0y, t1y)),
+                                   __builtin_fminf(t0z, t1z));
+  const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t0x, t1x), __builtin_fmaxf(t0y, t1y)),
+                                   __builtin_fmaxf(t0z, t1z));
+  b = (tn >= 0.0f) ? tn : tf;
+  return (tn <= tf) & (b < dist) & (b != -__builtin_inff());
+}
+
 // LDS byte offsets are 32-bit: keep the address arithmetic in 32 bits.
 __device__ __forceinline__ float4 lds4(uint32_t byte_off) {
   return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(g_smem) + byte_off);
@@ -353,6 +369,8 @@ __device__ __forceinline__ void trav_leaf(const KParams& kp, Counters& c, Trav& 
   t.active = !stop;
   t.ref = (t.cnt == 0 || stop) ? kNoneRef : t.ref;
   t.cnt = stop ? 0u : t.cnt;
+  t.sp = stop ? 0 : t.sp;  // a stopped shadow ray pops nothing (trav_pop tests no `active`)
+  if constexpr (!LDSM) t.lo = stop ? 0 : t.lo;
 }
 
 // Internal sub-step: test both children's boxes; push c0 when both pass, go to
@@ -363,9 +381,9 @@ __device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln,
   const float4 l0 = node4<LDSM>(kp, pi), h0 = node4<LDSM>(kp, pi + 1);
   const float4 l1 = node4<LDSM>(kp, pi + 2), h1 = node4<LDSM>(kp, pi + 3);
   bump<COUNT>(c, ST_NODES, 2);
-  const float b0 = box_t(t.o, t.inv, l0, h0);
-  const float b1 = box_t(t.o, t.inv, l1, h1);
-  const bool v0 = box_ok(b0, t.dist), v1 = box_ok(b1, t.dist);
+  float b0, b1;
+  const bool v0 = box_test(t.o, t.inv, l0, h0, t.dist, b0);
+  const bool v1 = box_test(t.o, t.inv, l1, h1, t.dist, b1);
   const uint32_t r0 = __float_as_uint(l0.w), n0 = __float_as_uint(h0.w);
   // the c0 slot is written unconditionally (it is free either way; the stack
   // holds depth + 1 entries, validated at upload)
@@ -392,11 +410,13 @@ __device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln,
 // Nothing current: pop one entry (visited if it still beats the running
 // distance).  A lane whose stack is empty waits for trav_finish at the end of
 // the iteration (its later sub-steps have nothing to do either), so the pop
-// is one branch.  A lane whose next BVH is pending (`start`, set up at the
-// next iteration) does nothing.
+// is one branch.  The test is two compares: ref == kNoneRef implies cnt == 0
+// (every update keeps it so), a shadow ray that stopped has emptied its
+// stack, and `start` is never set during the sub-steps (trav_finish sets it
+// at the end of an iteration, trav_step clears it before the first sub-step).
 template <bool LDSM, bool PACK>
 __device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav& t) {
-  if (t.active & !t.start & (t.cnt == 0) & (t.ref == kNoneRef) & (t.sp > 0)) {
+  if ((t.ref == kNoneRef) & (t.sp > 0)) {
     --t.sp;
     uint32_t r, n;
     float et;
@@ -418,7 +438,7 @@ __device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav
 // finished this BVH -- CheckHit's loop over bvh_count is complete (or, for a
 // shadow ray, a hit was found), or the next BVH is set up next iteration.
 __device__ __forceinline__ void trav_finish(const KParams& kp, Trav& t, bool any) {
-  if (t.active & !t.start & (t.cnt == 0) & (t.ref == kNoneRef) & (t.sp == 0)) {
+  if (t.active & (t.ref == kNoneRef) & (t.sp == 0)) {  // (see trav_pop for the short test)
     if ((any && t.hit != kNoneRef) || t.bi + 1 >= kp.bvh_count) {
       t.active = false;
     } else {
