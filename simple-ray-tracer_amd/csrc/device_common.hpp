@@ -34,6 +34,7 @@ struct KParams {
   int max_depth;
   int frame_first, nframes, write_output, reset;
   int rank, nranks, band_rows, local_rows;
+  int band_shift;          // log2(band_rows) when band_rows is a power of two, else -1
   int ext_w, ext_h;
   int stack_entries;
   int nodes_f4, tris_f4;   // LDS-resident scene: sizes of the node / triangle arrays in float4

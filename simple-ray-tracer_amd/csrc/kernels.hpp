@@ -124,7 +124,7 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
     bump<COUNT>(c, ST_RAYS);
     if (kp.show_model) {
       trav_begin_bvh<COUNT, LDSM>(kp, c, tr, ro, rd);
-      if (tr.cnt == 0 && tr.ref == kNoneRef) {  // root box missed: next BVH, or done
+      if (tr.cnt == kNoneCnt) {  // root box missed: next BVH, or done
         if (kp.bvh_count > 1) tr.start = true, tr.bi = 1;
         else tr.active = false;
       }
@@ -186,10 +186,16 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
         const int item = batch_next + r;
         const int px = tx * 8 + (item & 7), ly = ty * 8 + (item >> 3);
         if (px < kp.ext_w && ly < kp.local_rows) {
-          int band;
-          if (band_u >= 0) band = band_u;
-          else band = ly / kp.band_rows;
-          const int yy = (band * kp.nranks + kp.rank) * kp.band_rows + (ly - band * kp.band_rows);
+          // global row of local row ly: the identity on one rank; else by the
+          // row band (whole tiles: per batch; power-of-two bands: a shift)
+          int yy = ly;
+          if (kp.nranks > 1) {
+            int band;
+            if (band_u >= 0) band = band_u;
+            else if (kp.band_shift >= 0) band = ly >> kp.band_shift;
+            else band = ly / kp.band_rows;
+            yy = (band * kp.nranks + kp.rank) * kp.band_rows + (ly - band * kp.band_rows);
+          }
           if (yy < kp.ext_h) {  // else the item is outside the dispatch extent: the lane tries the next one
             fresh = true;
             a_pl = px | (ly << 16);
@@ -263,8 +269,8 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
         ++d_titers;
         d_work += __popcll(__ballot(has_work));
         d_trav += __popcll(trav);
-        d_leaf += __popcll(__ballot(tr.active && tr.cnt > 0));
-        d_int += __popcll(__ballot(tr.active && tr.cnt == 0 && tr.ref != kNoneRef));
+        d_leaf += __popcll(__ballot(tr.active && trav_at_leaf(tr.cnt)));
+        d_int += __popcll(__ballot(tr.active && tr.cnt == 0));
 #endif
         if (tr.active) trav_step<COUNT, LDSM, PACK>(kp, ln, c, tr, ro, rd, shadow_phase);
       }
@@ -297,7 +303,8 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
         if (kp.show_model) {
           rec.p = (dist * rd) + ro;
           const uint32_t ht = tr.hit;
-          const float4 A = tri4<LDSM>(kp, 3 * ht), B = tri4<LDSM>(kp, 3 * ht + 1), C = tri4<LDSM>(kp, 3 * ht + 2);
+          const float4* tp = tri_ptr<LDSM>(kp, ht);
+          const float4 A = tp[0], B = tp[1], C = tp[2];
           rec.normal = normalize(cross(mk(A.w, B.x, B.y), mk(B.z, B.w, C.x)));
           const uint32_t mi = __float_as_uint(C.y);
           float4 m0, m1;

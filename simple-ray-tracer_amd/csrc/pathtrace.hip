@@ -285,6 +285,9 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
   kp->rank = c->rank;
   kp->nranks = c->nranks;
   kp->band_rows = c->band_rows;
+  kp->band_shift = -1;
+  for (int s = 0; s < 31; ++s)
+    if ((1 << s) == c->band_rows) kp->band_shift = s;
   kp->local_rows = LocalRows(c, c->H);
   kp->local_pixels = kp->local_rows * c->W;
   kp->ext_w = c->W;
@@ -519,7 +522,7 @@ int ValidateNodes(const srt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_tris, 
       *max_depth = std::max(*max_depth, d);
       const srt_bvh_node& n = nodes[i];
       if (n.prim_count > 0) {
-        if ((uint64_t)n.first_child_or_prim_index + n.prim_count > n_tris) {
+        if ((uint64_t)n.first_child_or_prim_index + n.prim_count > n_tris || n.prim_count >= 0x80000000u) {
           srt::SetError("BVH leaf references triangles out of range");
           return SRT_ERR_INVALID;
         }

@@ -54,8 +54,9 @@ __device__ __forceinline__ float4 node4(const KParams& kp, uint32_t i) {
 // the records of triangle `i` onwards (3 float4 per triangle)
 template <bool LDSM>
 __device__ __forceinline__ const float4* tri_ptr(const KParams& kp, uint32_t i) {
-  if constexpr (LDSM)
-    return reinterpret_cast<const float4*>(reinterpret_cast<const char*>(g_smem) + (((uint32_t)kp.nodes_f4 + 3 * i) << 4));
+  if constexpr (LDSM)  // i < 2^24 in LDS mode: one v_mad_u32_u24 (a 32-bit mul + add becomes a slow v_mad_u64_u32)
+    return reinterpret_cast<const float4*>(reinterpret_cast<const char*>(g_smem) + ((uint32_t)kp.nodes_f4 * 16u +
+                                                                                  __umul24(i, 48u)));
   else return kp.tris + 3 * (size_t)i;
 }
 template <bool LDSM>
@@ -279,7 +280,8 @@ __device__ uint32_t trace_mesh(const KParams& kp, const Lane& ln, Counters& c, f
 struct Trav {
   f3 o, d, inv;       // ray in the current BVH's frame
   float dist;         // running intersection_distance
-  uint32_t ref, cnt;  // current node (leaf: first triangle + remaining; internal: first child)
+  uint32_t ref, cnt;  // current node: leaf (cnt > 0): first triangle + remaining; internal (cnt == 0):
+                      // first child; nothing current: cnt == kNoneCnt (ref is then unused)
   uint32_t hit;       // best triangle so far (0xFFFFFFFF: none)
   uint32_t bi;        // current BVH
   int sp;
@@ -289,6 +291,12 @@ struct Trav {
 };
 
 constexpr uint32_t kNoneRef = 0xFFFFFFFFu;
+// Trav::cnt of "nothing current, pop next": one compare tells the three states
+// apart (leaf: (int)cnt > 0; internal: cnt == 0; none: cnt == kNoneCnt), and
+// ref needs no update when a lane runs out of nodes.  Leaf counts are < 2^31
+// (srt_upload_scene validates it).
+constexpr uint32_t kNoneCnt = 0xFFFFFFFFu;
+__device__ __forceinline__ bool trav_at_leaf(uint32_t cnt) { return (int)cnt > 0; }
 #ifndef SRT_LEAF_TRIS
 #define SRT_LEAF_TRIS 2
 #endif
@@ -325,8 +333,8 @@ __device__ __forceinline__ void trav_begin_bvh(const KParams& kp, Counters& c, T
   const float4 rlo = node4<LDSM>(kp, 2 * root + 2), rhi = node4<LDSM>(kp, 2 * root + 3);
   bump<COUNT>(c, ST_NODES);
   const bool ok = box_ok(box_t(t.o, t.inv, rlo, rhi), t.dist);
-  t.ref = ok ? __float_as_uint(rlo.w) : kNoneRef;
-  t.cnt = ok ? __float_as_uint(rhi.w) : 0u;
+  t.ref = __float_as_uint(rlo.w);
+  t.cnt = ok ? __float_as_uint(rhi.w) : kNoneCnt;
   t.sp = 0;
   t.lo = 0;
   t.start = false;
@@ -365,10 +373,9 @@ __device__ __forceinline__ void trav_leaf(const KParams& kp, Counters& c, Trav& 
   t.dist = dist;
   t.hit = hit;
   t.ref += n;
-  t.cnt -= n;
+  const uint32_t rest = t.cnt - n;
   t.active = !stop;
-  t.ref = (t.cnt == 0 || stop) ? kNoneRef : t.ref;
-  t.cnt = stop ? 0u : t.cnt;
+  t.cnt = (rest == 0 || stop) ? kNoneCnt : rest;
   t.sp = stop ? 0 : t.sp;  // a stopped shadow ray pops nothing (trav_pop tests no `active`)
   if constexpr (!LDSM) t.lo = stop ? 0 : t.lo;
 }
@@ -403,20 +410,20 @@ __device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln,
   if constexpr (COUNT) {
     if ((uint32_t)t.sp > c.v[ST_MAXSTACK]) c.v[ST_MAXSTACK] = (uint32_t)t.sp;
   }
-  t.ref = v1 ? __float_as_uint(l1.w) : (v0 ? r0 : kNoneRef);
-  t.cnt = v1 ? __float_as_uint(h1.w) : (v0 ? n0 : 0u);
+  t.ref = v1 ? __float_as_uint(l1.w) : r0;
+  t.cnt = v1 ? __float_as_uint(h1.w) : (v0 ? n0 : kNoneCnt);
 }
 
 // Nothing current: pop one entry (visited if it still beats the running
 // distance).  A lane whose stack is empty waits for trav_finish at the end of
 // the iteration (its later sub-steps have nothing to do either), so the pop
-// is one branch.  The test is two compares: ref == kNoneRef implies cnt == 0
-// (every update keeps it so), a shadow ray that stopped has emptied its
-// stack, and `start` is never set during the sub-steps (trav_finish sets it
-// at the end of an iteration, trav_step clears it before the first sub-step).
+// is one branch.  The test is two compares: a shadow ray that stopped has
+// emptied its stack, and `start` is never set during the sub-steps
+// (trav_finish sets it at the end of an iteration, trav_step clears it before
+// the first sub-step).
 template <bool LDSM, bool PACK>
 __device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav& t) {
-  if ((t.ref == kNoneRef) & (t.sp > 0)) {
+  if ((t.cnt == kNoneCnt) & (t.sp > 0)) {
     --t.sp;
     uint32_t r, n;
     float et;
@@ -429,8 +436,8 @@ __device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav
       slot_read<PACK>(ln.stk, ln.stride, t.sp & (kShortStack - 1), r, n, et);
     }
     const bool take = et < t.dist;
-    t.ref = take ? r : kNoneRef;
-    t.cnt = take ? n : 0u;
+    t.ref = r;
+    t.cnt = take ? n : kNoneCnt;
   }
 }
 
@@ -438,7 +445,7 @@ __device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav
 // finished this BVH -- CheckHit's loop over bvh_count is complete (or, for a
 // shadow ray, a hit was found), or the next BVH is set up next iteration.
 __device__ __forceinline__ void trav_finish(const KParams& kp, Trav& t, bool any) {
-  if (t.active & (t.ref == kNoneRef) & (t.sp == 0)) {  // (see trav_pop for the short test)
+  if (t.active & (t.cnt == kNoneCnt) & (t.sp == 0)) {  // (see trav_pop for the short test)
     if ((any && t.hit != kNoneRef) || t.bi + 1 >= kp.bvh_count) {
       t.active = false;
     } else {
@@ -452,13 +459,13 @@ template <bool COUNT, bool LDSM, bool PACK, int K>
 __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln, Counters& c, Trav& t, bool any) {
   if constexpr (kStepPattern[K] != 0) {
     if constexpr (kStepPattern[K] == 'I') {
-      DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K, t.cnt == 0 && t.ref != kNoneRef);
-      if (t.cnt == 0 && t.ref != kNoneRef) trav_internal<COUNT, LDSM, PACK>(kp, ln, c, t);
+      DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K, t.cnt == 0);
+      if (t.cnt == 0) trav_internal<COUNT, LDSM, PACK>(kp, ln, c, t);
     } else {
-      DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K, t.cnt > 0);
-      if (t.cnt > 0) trav_leaf<COUNT, LDSM>(kp, c, t, any);
+      DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K, trav_at_leaf(t.cnt));
+      if (trav_at_leaf(t.cnt)) trav_leaf<COUNT, LDSM>(kp, c, t, any);
     }
-    DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K + 2, t.active & !t.start & (t.cnt == 0) & (t.ref == kNoneRef));
+    DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K + 2, t.active & (t.cnt == kNoneCnt));
     trav_pop<LDSM, PACK>(kp, ln, t);
     trav_substeps<COUNT, LDSM, PACK, K + 1>(kp, ln, c, t, any);
   }
