@@ -122,7 +122,7 @@ struct srt_context {
   size_t lbuf_bytes = 0;
   size_t lbuf_cap = (size_t)16 << 30;  // SRT_SAMPLE_BUFFER_MB
   int tail_claims = 16;  // SRT_TAIL_CLAIMS: claims per wave before the end from which claims take one batch
-  int trav_frac16 = 8;                 // SRT_TRAV_FRAC16 (measured best on Rubik 1080p with 2-triangle leaf steps)
+  int trav_frac16 = 9;                 // SRT_TRAV_FRAC16 (measured best on Rubik 1080p with the 16-sub-step pattern)
   int num_cus = 256;
   // stats
   unsigned long long* d_stats = nullptr;

@@ -304,7 +304,7 @@ constexpr int kLeafTris = SRT_LEAF_TRIS;  // triangles tested per leaf step
 // Sub-steps of one traversal iteration: 'I' expands an internal node, 'L'
 // tests a leaf's next triangles; each is followed by a pop if nothing is current.
 #ifndef SRT_STEP_PATTERN
-#define SRT_STEP_PATTERN "ILILILIL"
+#define SRT_STEP_PATTERN "ILILILILILILILIL"
 #endif
 constexpr char kStepPattern[] = SRT_STEP_PATTERN;
 // global-scene mode: entries per lane kept in the LDS ring (power of two)
