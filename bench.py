@@ -7,12 +7,18 @@ the default workload is the same frame shape and sampling on the reference's
 shipped model scene (Rubik.obj, model camera, the 6 lights of src/main.cpp:584-589).
 
 A step = one full progressive render of the workload: the reset frame + `spp`
-sampled frames (one fused kernel launch) and, for N > 1, the RCCL gather of
-every rank's row bands to rank 0 plus the root-side assembly of the frame.
-Inputs (scene, noise buffers, lights) are resident in HBM before timing.
+sampled frames (one fused kernel launch) and, for N > 1, the gather of every
+rank's row bands to rank 0 (RCCL over xGMI) plus the root-side assembly of the
+frame.  Inputs (scene, noise buffers, lights) are resident in HBM before timing.
+
+A second leg ("global_scene") times the real-mesh path: a synthetic 1 M-triangle
+mesh (SURVEY.md 8d generator) too large for the LDS scene copy, traversed from
+HBM/L2, at 1920x1080 and 16 spp.  It is reported under "legs" with its own
+roofline; `value` is the main leg.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
+       (tests: --backend gloo --same-device runs N ranks on one GPU, staging through the host)
 """
 from __future__ import annotations
 
@@ -29,10 +35,17 @@ sys.path.insert(0, str(ROOT))
 
 import numpy as np  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters and LDS / wave sections)
+CLOCK_HZ = 2.4e9
+HBM_PEAK_GBS = 8000.0
+SIMDS = 256 * 4
+CUS = 256
+VALU_ISSUE_CYCLES = 2  # one wave64 VALU instruction per 2 cycles per SIMD-32
+VALU_PEAK_GIPS = SIMDS * CLOCK_HZ / VALU_ISSUE_CYCLES / 1e9  # 1228.8 G wave-instructions/s
+LDS_PEAK_GCPS = CUS * CLOCK_HZ / 1e9  # 614.4 G LDS-array cycles/s (one per CU per clock)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -46,7 +59,13 @@ def parse():
     ap.add_argument("--band-rows", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--no-global-leg", action="store_true", help="skip the 1 M-triangle global-scene leg")
+    ap.add_argument("--global-tris", type=int, default=1_000_000)
+    ap.add_argument("--global-spp", type=int, default=16)
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
+    ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (multi-rank tests on one GPU)")
+    ap.add_argument("--dump", default=None, help="rank 0 saves the assembled frame (npz) after the last step")
+    return ap.parse_args(argv)
 
 
 def algorithmic_bytes(st: dict) -> int:
@@ -88,116 +107,230 @@ def cpu_baseline(setup, spp_first: int, target_s: float) -> dict:
                       f"workload ({rays} rays, {secs:.1f} s)"}
 
 
-def load_traffic(workload: str):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary for this workload, if any."""
-    p = ROOT / "profiles" / "traffic.json"
+def load_counters(workload: str):
+    """Per-launch PMC counters of the workload's sample_kernel from the committed rocprofv3 passes
+    (profiles/counters.json, written by tools/pmc_roofline.py), or None."""
+    p = ROOT / "profiles" / "counters.json"
     if not p.exists():
         return None
     try:
-        d = json.loads(p.read_text())
-        v = d.get(workload)
-        return None if v is None else float(v["hbm_bytes_per_launch"])
+        return json.loads(p.read_text()).get(workload)
     except Exception:
         return None
 
 
-def main():
-    args = parse()
+def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str) -> dict:
+    """Roofs of the dominant kernel, fractions of the live kernel time (HIP events on the launch stream):
+    VALU issue (SQ_INSTS_VALU x 2 cycles per SIMD-32 over 1024 SIMDs), LDS-array cycles
+    (SQ_LDS_IDX_ACTIVE over 256 CUs), HBM (corrected FETCH_SIZE + WRITE_SIZE over 8 TB/s).  The counters
+    are per launch of this workload, from profiles/counters.json; `bound` is the highest fraction."""
+    k_s = k_ms * 1e-3
+    alg_gbs = alg_bytes / k_s / 1e9
+    r = {"kernel": kernel_name, "kernel_ms": round(k_ms, 3), "algorithmic_bytes_per_launch": int(alg_bytes),
+         "algorithmic_GBps": round(alg_gbs, 1)}
+    cnt = load_counters(workload)
+    if cnt is None:
+        r.update({"bound": "hbm", "achieved": round(alg_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": round(alg_gbs / HBM_PEAK_GBS, 5), "traffic": None,
+                  "note": "no committed PMC counters for this workload: SURVEY 8d algorithmic bytes / HBM peak"})
+        return r
+    valu_gips = cnt["SQ_INSTS_VALU"] / k_s / 1e9
+    lds_gcps = cnt["SQ_LDS_IDX_ACTIVE"] / k_s / 1e9
+    hbm_bytes = cnt["hbm_bytes"]
+    hbm_gbs = hbm_bytes / k_s / 1e9
+    roofs = {
+        "valu_issue": (valu_gips, VALU_PEAK_GIPS, "G VALU wave-instructions/s"),
+        "lds": (lds_gcps, LDS_PEAK_GCPS, "G LDS-array cycles/s"),
+        "hbm": (hbm_gbs, HBM_PEAK_GBS, "GB/s"),
+    }
+    fr = {k: a / p for k, (a, p, _) in roofs.items()}
+    bound = max(fr, key=fr.get)
+    a, p, u = roofs[bound]
+    r.update({
+        "bound": bound, "achieved": round(a, 2), "peak": p, "unit": u, "frac": round(a / p, 4),
+        "traffic": int(hbm_bytes),
+        "fractions": {k: round(v, 4) for k, v in fr.items()},
+        "valu_lane_utilisation": round(cnt["SQ_THREAD_CYCLES_VALU"] / (64.0 * cnt["SQ_INSTS_VALU"]), 4),
+        "useful_valu_frac": round(fr["valu_issue"] * cnt["SQ_THREAD_CYCLES_VALU"] / (64.0 * cnt["SQ_INSTS_VALU"]), 4),
+        "lds_bank_conflict_frac": round(cnt["SQ_LDS_BANK_CONFLICT"] / max(cnt["SQ_LDS_IDX_ACTIVE"], 1.0), 4),
+        "counters_source": cnt.get("source", ""),
+        "note": "frac = the bound roof's fraction at the live kernel time; per-launch counters from the committed "
+                "rocprofv3 passes of this workload (profiles/counters.json). The 2.4 GHz peak clock makes every "
+                "fraction a lower bound. algorithmic_GBps = SURVEY 8d bytes per launch / kernel time: the scene "
+                "is read from LDS/L2, so it is not an HBM rate.",
+    })
+    return r
+
+
+def build_setup(scene: str, W: int, H: int, spp: int, max_depth: int, synthetic_tris: int):
+    from srt_amd import render as R
+
+    if scene == "rubik":
+        models = [R.rubik_model(ROOT / "tests" / "golden" / "objects")]
+        show_model, wl = True, f"rubik_{W}x{H}_{spp}spp"
+    elif scene == "synthetic":
+        models = [R.synthetic_model(synthetic_tris)]
+        show_model, wl = True, f"synthetic{synthetic_tris}_{W}x{H}_{spp}spp"
+    else:
+        models, show_model, wl = None, False, f"spheres_{W}x{H}_{spp}spp"
+    if max_depth != 5:
+        wl += f"_depth{max_depth}"
+    return R.make_setup(W, H, show_model=show_model, models=models, max_depth=max_depth), wl
+
+
+class RankRun:
+    """One rank's share of a workload: its row bands (srt_set_tiling), its images in torch tensors, and
+    bench's step (clear + one fused launch of `spp` frames + the gather / assembly on N > 1)."""
+
+    def __init__(self, setup, spp, *, rank, world, device, band_rows, stream):
+        import torch
+
+        from srt_amd import parallel as PAR
+        from srt_amd import render as R
+
+        self.setup, self.spp, self.rank, self.world, self.band = setup, spp, rank, world, band_rows
+        self.dev = torch.device("cuda", device)
+        self.rdr = R.Renderer(setup, device=device, stream=stream.cuda_stream, rank=rank, nranks=world,
+                              band_rows=band_rows)
+        self.c = self.rdr.compute
+        W, H = setup.width, setup.height
+        self.rows_pad = PAR.rows_pad(H, band_rows, world)
+        self.accum_local = torch.zeros((self.rows_pad, W, 4), dtype=torch.float32, device=self.dev)
+        self.out_local = torch.zeros((self.rows_pad, W), dtype=torch.int32, device=self.dev)
+        self.c.set_image_buffers(self.accum_local.data_ptr(), self.out_local.data_ptr())
+        self.full_accum = self.full_out = None
+        if rank == 0 and world > 1:
+            self.full_accum = torch.empty((H, W, 4), dtype=torch.float32, device=self.dev)
+            self.full_out = torch.empty((H, W), dtype=torch.int32, device=self.dev)
+
+    def count(self) -> dict:
+        """Deterministic counting run (untimed): the work every step repeats."""
+        import torch
+
+        self.rdr.render(self.spp, count=True, write_output=True)
+        torch.cuda.synchronize(self.dev)
+        return self.c.stats()
+
+    def step(self):
+        from srt_amd import parallel as PAR
+
+        self.rdr.clear()
+        self.c.render_frames(2, self.spp, write_output=(self.world == 1), count=False)
+        self.rdr.accum_frames = self.spp + 1
+        if self.world > 1:  # the one exchange: every rank's radiance rows to rank 0 (RCCL over xGMI)
+            stacked = PAR.gather_bands(self.accum_local, dst=0)
+            if self.rank == 0:
+                self.c.assemble_bands(stacked.data_ptr(), self.world, self.rows_pad, self.band, self.spp + 1,
+                                      self.full_accum.data_ptr(), self.full_out.data_ptr())
+
+    def frame(self):
+        """Rank 0's frame after a step: (accum (H, W, 4) float32, sRGB8 (H, W, 4) uint8) on the host."""
+        import torch
+
+        torch.cuda.synchronize(self.dev)
+        if self.world > 1:
+            acc, out = self.full_accum, self.full_out
+        else:
+            acc, out = self.accum_local, self.out_local
+        H, W = self.setup.height, self.setup.width
+        return (acc[:H].cpu().numpy(), out[:H].cpu().numpy().view(np.uint8).reshape(H, W, 4))
+
+    def close(self):
+        self.rdr.close()
+
+
+def run_leg(setup, spp, args, *, rank, world, device, stream):
+    """Counting run, warmup, then exactly `steps` timed steps bracketed by barrier + synchronize;
+    returns (elapsed max over ranks, total rays over ranks, this rank's stats, kernel ms list, run)."""
+    import torch
+    import torch.distributed as dist
+
+    run = RankRun(setup, spp, rank=rank, world=world, device=device, band_rows=args.band_rows, stream=stream)
+    st = run.count()
+    counts = torch.tensor([float(st["rays"])], dtype=torch.float64)
+    if world > 1:
+        counts = counts.to(run.dev) if args.backend == "nccl" else counts
+        dist.all_reduce(counts)
+    total_rays = float(counts[0].item())
+    for _ in range(args.warmup):
+        run.step()
+    torch.cuda.synchronize(run.dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(run.dev)
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run.step()
+        torch.cuda.synchronize(run.dev)
+        kernel_ms.append(run.c.last_kernel_ms())  # HIP events around sample_kernel on the launch stream
+    torch.cuda.synchronize(run.dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64)
+    if world > 1:
+        elapsed = elapsed.to(run.dev) if args.backend == "nccl" else elapsed
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    return float(elapsed.item()), total_rays, st, kernel_ms, run
+
+
+KERNEL_LDS = "srt::sample_kernel<false, true, true, 1024, false> (LDS-resident scene)"
+KERNEL_GLOBAL = "srt::sample_kernel<false, false, true, 256, false> (global-scene mode)"
+
+
+def main(argv=None):
+    args = parse(argv)
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    torch.cuda.set_device(local_rank)
+    if world != args.gpus and world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    device = 0 if args.same_device else local_rank
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-
-    import srt_amd as S
-    from srt_amd import render as R
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
 
     W, H, spp = args.width, args.height, args.spp
-    if args.scene == "rubik":
-        models = [R.rubik_model(ROOT / "tests" / "golden" / "objects")]
-        show_model, wl_name = True, f"rubik_{W}x{H}_{spp}spp"
-    elif args.scene == "synthetic":
-        models = [R.synthetic_model(args.synthetic_tris)]
-        show_model, wl_name = True, f"synthetic{args.synthetic_tris}_{W}x{H}_{spp}spp"
-    else:
-        models, show_model, wl_name = None, False, f"spheres_{W}x{H}_{spp}spp"
-    if args.max_depth != 5:
-        wl_name += f"_depth{args.max_depth}"
-    setup = R.make_setup(W, H, show_model=show_model, models=models, max_depth=args.max_depth)
-
-    dev = torch.device("cuda", local_rank)
+    setup, wl_name = build_setup(args.scene, W, H, spp, args.max_depth, args.synthetic_tris)
+    dev = torch.device("cuda", device)
     stream = torch.cuda.Stream(device=dev)   # a real (non-null) stream shared by torch and the library
     torch.cuda.set_stream(stream)
-    rdr = R.Renderer(setup, device=local_rank, stream=stream.cuda_stream, rank=rank, nranks=world,
-                     band_rows=args.band_rows)
-    c = rdr.compute
-    from srt_amd import parallel as PAR
 
-    rows_pad = PAR.rows_pad(H, args.band_rows, world)
-    local_rows = c.local_rows()
-    accum_local = torch.zeros((rows_pad, W, 4), dtype=torch.float32, device=dev)
-    out_local = torch.zeros((rows_pad, W), dtype=torch.int32, device=dev)
-    c.set_image_buffers(accum_local.data_ptr(), out_local.data_ptr())
-    if rank == 0 and world > 1:
-        full_accum = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
-        full_out = torch.empty((H, W), dtype=torch.int32, device=dev)
+    elapsed_s, total_rays, st, kernel_ms, run = run_leg(setup, spp, args, rank=rank, world=world, device=device,
+                                                        stream=stream)
+    if args.dump and rank == 0:
+        acc, out = run.frame()
+        np.savez(args.dump, accum=acc, out=out)
+    run.close()
 
-    # deterministic counting run (untimed): the work every step repeats
-    rdr.render(spp, count=True, write_output=True)
-    torch.cuda.synchronize()
-    st = c.stats()
-    counts = torch.tensor([st[k] for k in ("rays", "nodes", "tris", "rng_u", "rng_sq", "light_reads", "mat_reads",
-                                           "samples")], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(counts)
-    total_rays = float(counts[0].item())
-    local_bytes = algorithmic_bytes(st)
-
-    kernel_ms = []
-
-    def step(timed: bool):
-        rdr.clear()
-        c.render_frames(2, spp, write_output=(world == 1), count=False)
-        rdr.accum_frames = spp + 1
-        if world > 1:  # the one exchange: every rank's radiance rows to rank 0 (RCCL over xGMI)
-            stacked = PAR.gather_bands(accum_local, dst=0)
-            if rank == 0:
-                c.assemble_bands(stacked.data_ptr(), world, rows_pad, args.band_rows, spp + 1,
-                                 full_accum.data_ptr(), full_out.data_ptr())
-
-    for _ in range(args.warmup):
-        step(False)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-        torch.cuda.synchronize()
-        kernel_ms.append(c.last_kernel_ms())  # HIP events around sample_kernel on the launch stream
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed_s = float(elapsed.item())
+    legs = []
+    if not args.no_global_leg:
+        gsetup, gname = build_setup("synthetic", 1920, 1080, args.global_spp, 5, args.global_tris)
+        g_el, g_rays, g_st, g_kms, g_run = run_leg(gsetup, args.global_spp, args, rank=rank, world=world,
+                                                   device=device, stream=stream)
+        g_run.close()
+        if rank == 0:
+            g_k = float(np.mean(g_kms))
+            legs.append({
+                "leg": "global_scene", "workload": gname, "value": round(g_rays * args.steps / g_el / 1e6, 3),
+                "unit": "Mrays/s", "ms_per_step": round(g_el * 1e3 / args.steps, 3),
+                "config": {"scene": f"synthetic {args.global_tris} triangles (SURVEY 8d generator)", "width": 1920,
+                           "height": 1080, "spp": args.global_spp, "max_depth": 5},
+                "roofline": roofline(gname, g_k, algorithmic_bytes(g_st) if world == 1 else 0, KERNEL_GLOBAL),
+            })
 
     if rank == 0:
         ms_per_step = elapsed_s * 1e3 / args.steps
         value = total_rays * args.steps / elapsed_s / 1e6
         k_ms = float(np.mean(kernel_ms))
-        achieved = local_bytes / (k_ms * 1e-3) / 1e9
-        traffic = load_traffic(wl_name) if world == 1 else None
+        kname = KERNEL_LDS if args.scene == "rubik" else "srt::sample_kernel<false, ...>"
         line = {
             "metric": "Mrays/s (CheckHit queries: camera + bounce + shadow rays) at the BASELINE frame/spp",
             "value": round(value, 3),
@@ -216,34 +349,23 @@ def main():
             "config": {
                 "workload": wl_name, "width": W, "height": H, "spp": spp, "max_depth": args.max_depth,
                 "scene": args.scene, "lights": int(len(setup.lights)),
-                "parallelism": f"row-band tiling x{world} ({args.band_rows}-row bands) + RCCL gather" if world > 1
-                else "single GPU",
+                "parallelism": f"row-band tiling x{world} ({args.band_rows}-row bands) + gather to rank 0 "
+                               f"({'RCCL' if args.backend == 'nccl' else 'gloo'})" if world > 1 else "single GPU",
             },
             "frame_ms": round(ms_per_step / spp, 4),
             "msamples_per_s": round(W * H * spp * args.steps / elapsed_s / 1e6, 3),
             "rays_per_step": int(total_rays),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": traffic,
-                "kernel": "srt::sample_kernel<false, LDS, BLOCK> (HIP-event time per launch)",
-                "kernel_ms": round(k_ms, 3),
-                "algorithmic_bytes_per_launch": int(local_bytes),
-                "note": "SURVEY 8d bytes (node/triangle/material/noise/light reads) per launch / kernel time. "
-                        "The scene is read from its LDS copy and the noise from L2/MALL, so these bytes are not "
-                        "HBM traffic (measured HBM bytes: traffic) and frac > 1 means on-chip reuse. The kernel is "
-                        "bound by VALU issue under divergence (DESIGN.md section 5).",
-            },
+            # per-rank counters describe rank 0's launch: the roofline is a 1-GPU figure
+            "roofline": roofline(wl_name, k_ms, algorithmic_bytes(st), kname) if world == 1 else
+            {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
+             "kernel_ms": round(k_ms, 3), "note": "roofline reported at N=1"},
+            "legs": legs,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(setup, 2, args.cpu_seconds)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
-    rdr.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -44,8 +44,11 @@ inline Compute*& current() {
 }
 }  // namespace detail
 
-// Graphics::Compute: the raytrace_compute program.  `path` is kept for
-// interface parity; the kernel is built in (HIP code object for gfx950).
+// Graphics::Compute(path): the program is resolved as
+// Compute::CreateComputeProgram resolves it (srt_program_create: the file must
+// open; raytrace_compute.glsl is the path tracer, ray_intersects.glsl the
+// closest-hit test kernel); the kernels are HIP code objects for gfx950.
+// Init() throws where the reference std::terminate()s (Shader.cpp:125-157).
 class Compute {
  public:
   explicit Compute(const char* path, int device = 0, void* hip_stream = nullptr)
@@ -58,7 +61,15 @@ class Compute {
   Compute& operator=(const Compute&) = delete;
 
   void Init() {
+    if (!program_) {
+      program_ = srt_program_create(path_.c_str());
+      if (!program_) throw std::runtime_error("Compute::Init: no compute program for " + path_);
+    }
     if (!ctx_) check(srt_create(device_, stream_, &ctx_), "Compute::Init");
+  }
+  uint32_t program() {
+    Init();
+    return program_;
   }
   void Use() {
     Init();
@@ -108,6 +119,7 @@ class Compute {
   // glDispatchCompute(gx, gy, 1) (src/main.cpp:706); images 0/3 follow Width x Height
   void Dispatch(uint32_t gx, uint32_t gy, uint32_t gz = 1) {
     if (gz != 1) throw std::runtime_error("Dispatch: groups_z must be 1");
+    if (program() != SRT_PROGRAM_RAYTRACE) throw std::runtime_error("Dispatch: " + path_ + " is not raytrace_compute");
     if (images_dirty_) {
       check(srt_alloc_images(context()), "alloc images");
       images_dirty_ = false;
@@ -147,6 +159,7 @@ class Compute {
   int device_;
   void* stream_;
   srt_context* ctx_ = nullptr;
+  uint32_t program_ = 0;
   bool images_dirty_ = true;
   int width_ = 0;
 };
@@ -208,6 +221,7 @@ inline void UpdateModelMatrix(const uint32_t index, const std::array<float, 16>&
 inline std::vector<uint32_t> UpdateRaysAndTrace(const std::vector<srt_ray>& rays, std::vector<float>* t_out = nullptr) {
   Graphics::Compute* c = Graphics::detail::current();
   if (!c) throw std::runtime_error("UpdateRays: no Compute in use");
+  if (c->program() != SRT_PROGRAM_INTERSECT) throw std::runtime_error("UpdateRays: the program in use is not ray_intersects");
   std::vector<uint32_t> hits(rays.size());
   std::vector<float> t(rays.size());
   check(srt_trace_closest(c->context(), rays.data(), (uint32_t)rays.size(), hits.data(), t.data()), "UpdateRays");

@@ -75,6 +75,21 @@ int srt_abi_version(void);
  * (include/compute/create_compute_program.h:46-72).  `stream` is a
  * hipStream_t (NULL = the context creates its own). */
 int srt_create(int device, void* stream, srt_context** out);
+
+/* Compute::CreateComputeProgram (include/compute/create_compute_program.h:46-72):
+ * a program handle, or 0 with the log on stderr as the reference prints it
+ * ("err opening<path>" when the file cannot be opened, :13-16; "compile
+ * error:" for a program with no MI355X kernel, :31-40).  The program is the
+ * file's basename: raytrace_compute.glsl -> SRT_PROGRAM_RAYTRACE (the path
+ * tracer, srt_dispatch / srt_render_frames), ray_intersects.glsl ->
+ * SRT_PROGRAM_INTERSECT (the closest-hit test kernel, srt_trace_closest).
+ * "builtin:raytrace_compute" / "builtin:ray_intersects" name them without a
+ * file.  The GLSL text is not compiled: the kernels are HIP code objects. */
+#define SRT_PROGRAM_RAYTRACE 1u
+#define SRT_PROGRAM_INTERSECT 2u
+uint32_t srt_program_create(const char* path);
+/* glDeleteProgram: SRT_OK for a handle srt_program_create returned, else SRT_ERR_INVALID. */
+int srt_program_delete(uint32_t program);
 int srt_destroy(srt_context* ctx);
 void* srt_stream(srt_context* ctx);
 
@@ -193,6 +208,21 @@ int srt_model_from_triangles(const float* xyz9, uint32_t n_tris, const float kd[
 int srt_model_free(srt_model* m);
 /* counts: [0]=triangles [1]=vertices [2]=nodes [3]=leaves [4]=max depth [5]=materials [6]=faces dropped */
 int srt_model_info(const srt_model* m, uint64_t counts[8], float root_min[3], float root_max[3]);
+/* One model's host arrays in the reference's AssetUtils::Model shape, before
+ * UploadModelDataToGPU flattens them (indices local to the model):
+ * model_bvh.GetBVH() nodes (intersection_utils/bvh.h:23-30), GetPrims()
+ * (asset_utils/types.h:25-28), model_materials (types.h:31-37; tex_albedo =
+ * the texture's sample at uv (0,0)) and vertex_data_buffer (types.h:17-23).
+ * A caller keeping the reference's own gpu_loader.cpp:63-133 flattening feeds
+ * the result to srt_upload_scene (tests/cpp/test_ref_loader.cpp). */
+typedef struct { float min_bounds[3]; float max_bounds[3];
+                 uint32_t first_child, first_prim_index, prim_count; } srt_host_bvh_node;   /* 36 B */
+typedef struct { float diffuse[3]; float specular[3]; float specular_ex; uint32_t use_texture;
+                 float tex_albedo[3]; } srt_host_material;                                  /* 44 B */
+/* sizes: [0]=nodes [1]=prims [2]=materials [3]=vertices */
+int srt_model_sizes(const srt_model* m, uint32_t sizes[4]);
+int srt_model_copy(const srt_model* m, srt_host_bvh_node* nodes, srt_triangle* prims, srt_host_material* mats,
+                   srt_vertex* verts);
 
 /* Flatten models exactly as UploadModelDataToGPU does (index rebasing). */
 int srt_scene_build(const srt_model* const* models, uint32_t n_models, srt_scene** out);

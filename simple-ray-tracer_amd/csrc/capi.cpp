@@ -1,5 +1,7 @@
 // capi.cpp -- C ABI of the host-side scene producers (include/srt_amd.h).
 #include <cstring>
+#include <fstream>
+#include <iostream>
 #include <string>
 #include <vector>
 
@@ -26,6 +28,40 @@ int srt_model_load_ex(const char* obj_path, uint32_t flags, srt_model** out) {
   }
   *out = new srt_model{std::move(m)};
   return SRT_OK;
+}
+
+uint32_t srt_program_create(const char* path) {
+  // create_compute_program.h:10-72: 0 with the log on stderr on failure
+  if (!path) {
+    std::cerr << "err opening(null)" << std::endl;
+    srt::SetError("CreateComputeProgram: null path");
+    return 0;
+  }
+  const std::string p(path);
+  std::string name;
+  if (p.rfind("builtin:", 0) == 0) {
+    name = p.substr(8);
+  } else {
+    std::ifstream f(p);
+    if (!f.is_open()) {  // LoadComputeShader, :13-16
+      std::cerr << "err opening" << p << std::endl;
+      srt::SetError("CreateComputeProgram: cannot open " + p);
+      return 0;
+    }
+    const size_t slash = p.find_last_of('/');
+    name = p.substr(slash == std::string::npos ? 0 : slash + 1);
+    const size_t dot = name.rfind(".glsl");
+    if (dot != std::string::npos && dot + 5 == name.size()) name.resize(dot);
+  }
+  if (name == "raytrace_compute") return SRT_PROGRAM_RAYTRACE;
+  if (name == "ray_intersects") return SRT_PROGRAM_INTERSECT;
+  std::cerr << "compile error:\nno MI355X kernel for compute program '" << name << "' (" << p << ")" << std::endl;
+  srt::SetError("CreateComputeProgram: no kernel for " + p);
+  return 0;
+}
+
+int srt_program_delete(uint32_t program) {
+  return (program == SRT_PROGRAM_RAYTRACE || program == SRT_PROGRAM_INTERSECT) ? SRT_OK : SRT_ERR_INVALID;
 }
 
 int srt_model_from_triangles(const float* xyz9, uint32_t n_tris, const float kd[3], const float ks[3], float ns,
@@ -60,6 +96,52 @@ int srt_model_info(const srt_model* mm, uint64_t counts[8], float root_min[3], f
       root_max[0] = m.nodes[0].max_bounds.x; root_max[1] = m.nodes[0].max_bounds.y; root_max[2] = m.nodes[0].max_bounds.z;
     }
   }
+  return SRT_OK;
+}
+
+int srt_model_sizes(const srt_model* mm, uint32_t sizes[4]) {
+  if (!mm || !mm->m || !sizes) return SRT_ERR_INVALID;
+  const srt::Model& m = *mm->m;
+  sizes[0] = (uint32_t)m.nodes.size();
+  sizes[1] = (uint32_t)m.prims.size();
+  sizes[2] = (uint32_t)m.materials.size();
+  sizes[3] = (uint32_t)m.vertices.size();
+  return SRT_OK;
+}
+
+int srt_model_copy(const srt_model* mm, srt_host_bvh_node* nodes, srt_triangle* prims, srt_host_material* mats,
+                   srt_vertex* verts) {
+  if (!mm || !mm->m) return SRT_ERR_INVALID;
+  const srt::Model& m = *mm->m;
+  if (nodes)
+    for (size_t i = 0; i < m.nodes.size(); ++i) {
+      const srt::BVHNode& n = m.nodes[i];
+      srt_host_bvh_node& o = nodes[i];
+      for (int k = 0; k < 3; ++k) {
+        o.min_bounds[k] = n.min_bounds[k];
+        o.max_bounds[k] = n.max_bounds[k];
+      }
+      o.first_child = n.first_child;
+      o.first_prim_index = n.first_prim_index;
+      o.prim_count = n.prim_count;
+    }
+  if (prims)
+    for (size_t i = 0; i < m.prims.size(); ++i)
+      prims[i] = srt_triangle{m.prims[i].vertex_idxs[0], m.prims[i].vertex_idxs[1], m.prims[i].vertex_idxs[2],
+                              m.prims[i].material_idx};
+  if (mats)
+    for (size_t i = 0; i < m.materials.size(); ++i) {
+      const srt::Material& a = m.materials[i];
+      srt_host_material& o = mats[i];
+      for (int k = 0; k < 3; ++k) {
+        o.diffuse[k] = a.diffuse[k];
+        o.specular[k] = a.specular[k];
+        o.tex_albedo[k] = a.tex_albedo[k];
+      }
+      o.specular_ex = a.specular_ex;
+      o.use_texture = a.use_texture ? 1u : 0u;
+    }
+  if (verts) std::memcpy(verts, m.vertices.data(), m.vertices.size() * sizeof(srt_vertex));
   return SRT_OK;
 }
 

@@ -271,11 +271,17 @@ class Compute:
         self.device = device
         self._stream = stream
         self._ctx = None
+        self.program = 0
         self.width = 0
         self.height = 0
 
     # -- lifecycle ----------------------------------------------------------
     def Init(self):
+        if not getattr(self, "program", 0):
+            # Compute::CreateComputeProgram (create_compute_program.h:46-72): 0 -> the reference terminates
+            self.program = int(lib().srt_program_create((self.path or "builtin:raytrace_compute").encode()))
+            if self.program == 0:
+                raise RuntimeError(f"Compute::Init: no compute program for {self.path!r}: {_lib.last_error()}")
         if self._ctx is None:
             h = C.c_void_p()
             check(lib().srt_create(self.device, C.c_void_p(self._stream) if self._stream else None, C.byref(h)),

@@ -20,6 +20,8 @@ SRT_ERR_NOT_FOUND = 3
 SRT_ERR_IO = 4
 SRT_ERR_STATE = 5
 SRT_ERR_LIMIT = 6
+SRT_PROGRAM_RAYTRACE = 1
+SRT_PROGRAM_INTERSECT = 2
 
 
 class BvhRecord(C.Structure):
@@ -78,6 +80,8 @@ _SIGS = {
     "srt_last_error": (C.c_char_p, []),
     "srt_abi_version": (C.c_int, []),
     "srt_create": (C.c_int, [C.c_int, P, C.POINTER(P)]),
+    "srt_program_create": (C.c_uint32, [C.c_char_p]),
+    "srt_program_delete": (C.c_int, [C.c_uint32]),
     "srt_destroy": (C.c_int, [P]),
     "srt_stream": (P, [P]),
     "srt_set_bool": (C.c_int, [P, C.c_char_p, C.c_int]),
@@ -115,6 +119,8 @@ _SIGS = {
     "srt_model_from_triangles": (C.c_int, [P, C.c_uint32, P, P, C.c_float, C.POINTER(P)]),
     "srt_model_free": (C.c_int, [P]),
     "srt_model_info": (C.c_int, [P, P, P, P]),
+    "srt_model_sizes": (C.c_int, [P, P]),
+    "srt_model_copy": (C.c_int, [P, P, P, P, P]),
     "srt_scene_build": (C.c_int, [P, C.c_uint32, C.POINTER(P)]),
     "srt_scene_free": (C.c_int, [P]),
     "srt_scene_sizes": (C.c_int, [P, P]),

@@ -49,6 +49,13 @@ def gather_bands(local, dst: int = 0):
     rank = dist.get_rank()
     if world == 1:
         return local.unsqueeze(0)
-    parts = [torch.empty_like(local) for _ in range(world)] if rank == dst else None
-    dist.gather(local, parts, dst=dst)
-    return torch.stack(parts) if rank == dst else None
+    # gloo gathers host tensors: a device buffer is staged through the host and the stacked result
+    # moved back (multi-rank tests on one GPU); RCCL ("nccl") gathers device memory directly over xGMI
+    staged = dist.get_backend() == "gloo" and local.is_cuda
+    src = local.cpu() if staged else local
+    parts = [torch.empty_like(src) for _ in range(world)] if rank == dst else None
+    dist.gather(src, parts, dst=dst)
+    if rank != dst:
+        return None
+    stacked = torch.stack(parts)
+    return stacked.to(local.device) if staged else stacked

@@ -1,6 +1,8 @@
 // test_api.cpp -- the reference's GL integration test (include/compute/tests/BVH_intergration_tests.cpp)
 // and src/main.cpp's progressive loop, written against the C++ mirror API (include/srt/srt.hpp).
-// Run on a GPU box: ./test_api <objects_dir>; prints "OK <checksum>" on success.
+// Run on a GPU box: ./test_api <objects_dir> <shader_dir> <out_prefix>; prints "OK <checksum>" on
+// success and writes the progressive loop's accumulation image (<out_prefix>.accum, RGBA32F rows) and
+// sRGB8 image (<out_prefix>.rgba8) for tests/test_gpu_parity.py to compare with the CPU oracle.
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -18,8 +20,14 @@ static int fail(const char* what) {
 
 int main(int argc, char** argv) {
   const std::string objects = argc > 1 ? argv[1] : "./objects/";
+  const std::string shaders = argc > 2 ? argv[2] : "./shaders/";
+  const std::string out_prefix = argc > 3 ? argv[3] : "";
+  // --- Compute::CreateComputeProgram's contract (create_compute_program.h:46-72): 0 on failure ---
+  if (srt_program_create((shaders + "missing.glsl").c_str()) != 0) return fail("missing shader file accepted");
+  if (srt_program_create((shaders + "ray_intersects.glsl").c_str()) != SRT_PROGRAM_INTERSECT)
+    return fail("ray_intersects.glsl");
   // --- BVH_intergration_tests.cpp:63-116 ---
-  Graphics::Compute compute("./shaders/ray_intersects.glsl");
+  Graphics::Compute compute((shaders + "ray_intersects.glsl").c_str());
   compute.Use();
   auto model = AssetUtils::LoadObject("Rubik", objects);
   AssetUtils::UploadModelDataToGPU({model.get()});
@@ -53,7 +61,7 @@ int main(int argc, char** argv) {
 
   // --- src/main.cpp's progressive loop on a small frame ---
   const int W = 64, H = 48;
-  Graphics::Compute rt("./shaders/raytrace_compute.glsl");
+  Graphics::Compute rt((shaders + "raytrace_compute.glsl").c_str());
   rt.Use();
   rt.SetWidthHint(W);
   AssetUtils::UploadModelDataToGPU({model.get()}, 5);
@@ -85,6 +93,15 @@ int main(int argc, char** argv) {
     rt.Finish();
   }
   const auto out = rt.ReadOutput();
+  const auto acc = rt.ReadAccum();
+  if (!out_prefix.empty()) {
+    FILE* f = std::fopen((out_prefix + ".accum").c_str(), "wb");
+    if (!f || std::fwrite(acc.data(), sizeof(float), acc.size(), f) != acc.size()) return fail("write accum");
+    std::fclose(f);
+    f = std::fopen((out_prefix + ".rgba8").c_str(), "wb");
+    if (!f || std::fwrite(out.data(), 1, out.size(), f) != out.size()) return fail("write rgba8");
+    std::fclose(f);
+  }
   unsigned long long sum = 0;
   for (uint8_t b : out) sum = sum * 1315423911ull + b;
   std::printf("OK %llu\n", sum);

@@ -1,0 +1,183 @@
+"""GPU parity at BASELINE.json's configurations (C1, C2, C4, C5) and on the kernel instances the
+small-scene tests do not reach.
+
+Bar (as in test_gpu_parity.py): the HIP accumulation image bit-identical to the CPU oracle (NaN ==
+NaN), the RGBA8 image identical.  Where a full-frame oracle render would take minutes, the oracle
+renders rows spread across the frame at the config's full spp, and size-independent properties
+cover the rest: determinism of two full renders, and the 8-rank row-band split (rendered rank by
+rank on one GPU, reassembled by srt_assemble_bands) bit-identical to the 1-rank frame.
+
+Configs (BASELINE.json "configs"):
+  C1 sphere scene 256x256 @ 1 spp (maxDepth 5)              -- full frame vs the oracle
+  C2 sphere scene 1024x1024 @ 64 spp, maxDepth 4            -- full render, oracle rows
+  C3 Airplane OBJ 1920x1080 @ 256 spp                       -- blocked: the .obj is absent from the
+                                                               reference checkout (.MISSING_LARGE_BLOBS);
+                                                               its materials are pinned by test_airplane_*
+  C4 Rubik 4096x4096 @ 1024 spp, maxDepth 8, 8 ranks        -- full render, oracle rows at 1024 spp,
+                                                               8-way band split reassembled
+  C5 synthetic 10 M triangles 4096x4096 (512 spp in the config) -- full frame at 2 spp, oracle rows,
+                                                               determinism
+"""
+import numpy as np
+import pytest
+
+import srt_amd as S
+from srt_amd import parallel as PAR
+from srt_amd import render as R
+from conftest import OBJECTS, bits_equal, oracle_render
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_render(setup, spp, **kw):
+    r = R.Renderer(setup, **kw)
+    try:
+        r.render(spp, count=True)
+        r.finish()
+        return r.accum(), r.output(), r.compute.stats()
+    finally:
+        r.close()
+
+
+def spread_rows(height, n):
+    """n rows spread over the frame, first and last included."""
+    return np.unique(np.linspace(0, height - 1, n).round().astype(np.int32))
+
+
+def assert_rows(gacc, gout, acc, out, rows):
+    eq = bits_equal(gacc[rows], acc[rows])
+    assert eq.all(), f"{(~eq).sum()} accumulation values differ on the sampled rows"
+    assert (gout[rows] == out[rows]).all()
+
+
+def test_c1_spheres_256_1spp_full_frame():
+    setup = R.make_setup(256, 256, show_model=False, max_depth=5)
+    acc, out, st = oracle_render(setup, 1)
+    gacc, gout, gst = gpu_render(setup, 1)
+    assert bits_equal(gacc, acc).all()
+    assert (gout == out).all()
+    assert gst["rays"] == st["rays"] and gst["samples"] == 256 * 256 and gst["stack_overflow"] == 0
+
+
+def test_c2_spheres_1024_64spp_depth4():
+    setup = R.make_setup(1024, 1024, show_model=False, max_depth=4)
+    gacc, gout, gst = gpu_render(setup, 64)
+    rows = spread_rows(1024, 24)
+    acc, out, st = oracle_render(setup, 64, rows=rows)
+    assert_rows(gacc, gout, acc, out, rows)
+    assert gst["samples"] == 1024 * 1024 * 64 and gst["stack_overflow"] == 0
+    assert np.isfinite(gacc[..., :3]).all() and (gacc[..., 3] == 1.0).all()
+
+
+def _assemble(setup, parts, band, spp):
+    """The root side of bench.py's step: srt_assemble_bands over the ranks' packed rows."""
+    import torch
+
+    W, H = setup.width, setup.height
+    nranks = len(parts)
+    rows_pad = PAR.rows_pad(H, band, nranks)
+    gathered = torch.zeros((nranks, rows_pad, W, 4), dtype=torch.float32, device="cuda")
+    for rank, loc in enumerate(parts):
+        gathered[rank, :loc.shape[0]] = torch.from_numpy(loc).cuda()
+    torch.cuda.synchronize()
+    r = R.Renderer(setup)
+    try:
+        acc = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+        out = torch.empty((H, W), dtype=torch.int32, device="cuda")
+        r.compute.assemble_bands(gathered.data_ptr(), nranks, rows_pad, band, spp + 1, acc.data_ptr(),
+                                 out.data_ptr())
+        r.finish()
+        torch.cuda.synchronize()
+        return acc.cpu().numpy(), out.cpu().numpy().view(np.uint8).reshape(H, W, 4)
+    finally:
+        r.close()
+
+
+def test_c4_rubik_4096_1024spp_depth8_rows_and_8_rank_split():
+    W = H = 4096
+    spp = 1024
+    setup = R.make_setup(W, H, show_model=True, models=[R.rubik_model(OBJECTS)], max_depth=8)
+    gacc, gout, gst = gpu_render(setup, spp)
+    assert gst["samples"] == W * H * spp and gst["stack_overflow"] == 0
+    rows = spread_rows(H, 16)
+    acc, out, _ = oracle_render(setup, spp, rows=rows)
+    assert_rows(gacc, gout, acc, out, rows)
+    # the 8-GPU split of the config, rank by rank on one GPU (bench.py's 2-row bands)
+    band, nranks = 2, 8
+    parts = [gpu_render(setup, spp, rank=r, nranks=nranks, band_rows=band)[0] for r in range(nranks)]
+    facc, fout = _assemble(setup, parts, band, spp)
+    assert bits_equal(facc, gacc).all()
+    assert (fout == gout).all()
+
+
+@pytest.fixture(scope="module")
+def c5_setup():
+    model = R.synthetic_model(10_000_000)
+    info = model.info()
+    assert info["triangles"] == 10_000_000
+    return R.make_setup(4096, 4096, show_model=True, models=[model])
+
+
+def test_c5_synthetic_10M_rows_and_determinism(c5_setup):
+    """C5 at its full frame size and scene; 2 spp of its 512 (the rate, not the image, is the config's point)."""
+    setup = c5_setup
+    spp = 2
+    a, o, st = gpu_render(setup, spp)
+    assert st["samples"] == 4096 * 4096 * spp and st["stack_overflow"] == 0
+    assert st["max_stack"] > 0
+    rows = spread_rows(4096, 6)
+    acc, out, _ = oracle_render(setup, spp, rows=rows)
+    assert_rows(a, o, acc, out, rows)
+    b, p, st2 = gpu_render(setup, spp)
+    assert bits_equal(a, b).all() and (o == p).all()
+    assert st2["rays"] == st["rays"] and st2["nodes"] == st["nodes"] and st2["tris"] == st["tris"]
+
+
+def _coincident_star(n=300, seed=5):
+    """n triangles whose centroids are exactly (0, 6, 0): dyadic coordinates, so (p0 + p1 + p2) / 3
+    is exact and the midpoint split can never separate them -- one leaf of n >= 256 triangles
+    (bvh.h:129-130: a side is empty), which sends the scene to the unpacked 3-dword stack path."""
+    rng = np.random.default_rng(seed)
+    c = np.array([0.0, 6.0, 0.0], np.float32)
+    a = rng.integers(-24, 25, size=(n, 3)).astype(np.float32) / np.float32(8.0)
+    b = rng.integers(-24, 25, size=(n, 3)).astype(np.float32) / np.float32(8.0)
+    tri = np.stack([c + a, c + b, c - a - b], axis=1)
+    floor = np.array([[-30, 0, -30], [30, 0, -30], [30, 0, 30], [-30, 0, -30], [30, 0, 30], [-30, 0, 30]],
+                     np.float32).reshape(2, 3, 3)
+    return np.concatenate([floor, tri]).reshape(-1, 9)
+
+
+def test_unpacked_stack_path_big_leaf():
+    """A leaf of >= 256 triangles: global-scene mode with 3-dword (unpacked) stack entries."""
+    model = S.model_from_triangles(_coincident_star(), kd=(0.7, 0.6, 0.5), ks=(0.2, 0.2, 0.2), ns=20.0)
+    setup = R.make_setup(48, 40, show_model=True, models=[model])
+    assert int(setup.scene.nodes["count"].max()) >= 256
+    setup.camera.position = np.asarray((0.0, 7.0, 14.0), np.float32)
+    acc, out, st = oracle_render(setup, 3)
+    gacc, gout, gst = gpu_render(setup, 3)
+    assert bits_equal(gacc, acc).all()
+    assert (gout == out).all()
+    assert gst["rays"] == st["rays"] and gst["tris"] == st["tris"] and gst["nodes"] == st["nodes"]
+
+
+def test_unpacked_stack_path_closest_hit():
+    from oracle import pyoracle as O
+
+    model = S.model_from_triangles(_coincident_star(), kd=(0.7, 0.6, 0.5), ks=(0.2, 0.2, 0.2), ns=20.0)
+    scene = S.Scene.from_models([model])
+    rng = np.random.default_rng(3)
+    rays = np.zeros(4000, S.RAY_DTYPE)
+    rays["o"] = rng.uniform([-8, 1, -8], [8, 12, 8], size=(4000, 3)).astype(np.float32)
+    tgt = np.array([0.0, 6.0, 0.0], np.float32) + rng.normal(scale=1.5, size=(4000, 3)).astype(np.float32)
+    rays["d"] = (tgt - rays["o"]).astype(np.float32)
+    rays["t"] = np.float32(1e30)
+    hits_o, t_o, _, _ = O.Oracle(scene).trace_closest(1, rays)
+    c = S.Compute().Init()
+    try:
+        c.bind_scene(scene)
+        c.SetUInt("bvh_count", 1)
+        hits, t = c.trace_closest(rays)
+    finally:
+        c.close()
+    assert (hits == hits_o).all() and bits_equal(t, t_o).all()
+    assert (hits >= 2).sum() > 1000  # most rays hit the coincident leaf, not the floor

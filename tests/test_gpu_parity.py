@@ -227,7 +227,7 @@ def test_schedule_invariance(rubik, monkeypatch):
             monkeypatch.delenv(k)
 
 
-@pytest.mark.parametrize("nranks,band", [(2, 16), (3, 8)])
+@pytest.mark.parametrize("nranks,band", [(2, 16), (3, 8), (2, 2), (3, 3), (8, 2), (5, 1)])
 def test_row_band_tiling_reassembles(rubik, nranks, band):
     import torch
 
@@ -300,14 +300,25 @@ def test_full_frame_rows_and_determinism(rubik):
     assert np.isfinite(a[..., :3]).mean() > 0.999 and (a[..., 3] == 1.0).all()
 
 
-def test_cpp_api_program():
-    """The C++ mirror API running the reference's integration test + main loop (tests/cpp/test_api.cpp)."""
+def test_cpp_api_program(rubik, tmp_path):
+    """The C++ mirror API running the reference's integration test + main loop (tests/cpp/test_api.cpp);
+    the loop's frame (reset + 3 sampled frames of Rubik at 64x48) is checked against the oracle."""
     exe = ROOT / "tests" / "cpp" / "_build" / "test_api"
     exe.parent.mkdir(exist_ok=True)
     subprocess.run(["g++", "-std=c++17", "-O1", "-I", str(ROOT / "include"), str(ROOT / "tests/cpp/test_api.cpp"),
                     "-o", str(exe), "-L", str(PKG), "-lsrt_amd", f"-Wl,-rpath,{PKG}"], check=True)
-    res = subprocess.run([str(exe), str(OBJECTS) + "/"], capture_output=True, text=True, timeout=120)
+    shaders = tmp_path / "shaders"
+    shaders.mkdir()
+    for name in ("raytrace_compute.glsl", "ray_intersects.glsl"):  # CreateComputeProgram opens the file
+        (shaders / name).write_text("#version 450\n")
+    res = subprocess.run([str(exe), str(OBJECTS) + "/", str(shaders) + "/", str(tmp_path / "loop")],
+                         capture_output=True, text=True, timeout=120)
     assert res.returncode == 0 and res.stdout.startswith("OK"), res.stdout + res.stderr
+    acc = np.fromfile(tmp_path / "loop.accum", np.float32).reshape(48, 64, 4)
+    out = np.fromfile(tmp_path / "loop.rgba8", np.uint8).reshape(48, 64, 4)
+    want_acc, want_out, _ = oracle_render(R.make_setup(64, 48, show_model=True, models=[rubik]), 3)
+    assert bits_equal(acc, want_acc).all()
+    assert (out == want_out).all()
 
 
 def test_save_image_matches_output(rubik, tmp_path):
@@ -342,3 +353,22 @@ def test_moved_camera_spheres_parity():
     setup.camera.Rotate(-35.0, 20.0)
     setup.camera.position = np.asarray((1.5, 0.5, 2.0), np.float32)
     assert_parity(setup, 3)
+
+
+def test_reference_upload_path_renders_oracle_frame(rubik, tmp_path):
+    """tests/cpp/test_ref_loader.cpp render: gpu_loader.cpp's own flattening handed to srt_upload_scene
+    (two Rubik models, the second moved by UpdateModelMatrix, bvh_count 2) renders the frame that
+    srt_upload_scene_obj renders, and that frame is the oracle's."""
+    from test_boundary import _build
+
+    exe = _build("test_ref_loader")
+    res = subprocess.run([str(exe), "render", str(OBJECTS) + "/", str(tmp_path / "ref")], capture_output=True,
+                         text=True, timeout=120)
+    assert res.returncode == 0 and res.stdout.startswith("OK render"), res.stdout + res.stderr
+    acc = np.fromfile(tmp_path / "ref.accum", np.float32).reshape(48, 64, 4)
+    setup = R.make_setup(64, 48, show_model=True, models=[rubik, S.load_obj(OBJECTS / "Rubik" / "Rubik.obj")])
+    frame = np.eye(4, dtype=np.float32)
+    frame[3, :3] = (12.0, -2.0, -5.0)
+    setup.scene.bvhs[1]["frame"] = frame.reshape(16)
+    want, _, _ = oracle_render(setup, 3)
+    assert bits_equal(acc, want).all()
