@@ -92,7 +92,10 @@ class Compute {
   void SetInt(const std::string& name, int v) {  // unknown names are silently ignored (Shader.cpp:190-205)
     const int rc = srt_set_int(context(), name.c_str(), v);
     if (rc != SRT_ERR_NOT_FOUND) check(rc, "SetInt");
-    if (rc == SRT_OK && (name == "Width" || name == "Height")) images_dirty_ = true;
+    // images 0/3 follow Width x Height: re-allocated (cleared) only when the size changes, as a
+    // GL texture keeps its contents across frames (src/main.cpp sets both every frame)
+    if (rc == SRT_OK && name == "Width" && v != img_w_) img_w_ = v, images_dirty_ = true;
+    if (rc == SRT_OK && name == "Height" && v != img_h_) img_h_ = v, images_dirty_ = true;
   }
   void SetUInt(const std::string& name, uint32_t v) {
     const int rc = srt_set_uint(context(), name.c_str(), v);
@@ -161,6 +164,7 @@ class Compute {
   srt_context* ctx_ = nullptr;
   uint32_t program_ = 0;
   bool images_dirty_ = true;
+  int img_w_ = -1, img_h_ = -1;
   int width_ = 0;
 };
 

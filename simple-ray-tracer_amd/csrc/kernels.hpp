@@ -582,14 +582,15 @@ __global__ __launch_bounds__(256) void reset_kernel(KParams kp) {
 }
 
 // The closest-hit test kernel of ray_intersects.glsl:135-161.
+// Stacks in LDS (stride = block), or lane-interleaved in HBM when `gstk` is given (deep trees).
 __global__ __launch_bounds__(256) void closest_kernel(KParams kp, const srt_ray* rays, uint32_t n, uint32_t* hits,
-                                                      float* tout) {
+                                                      float* tout, uint32_t* gstk) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Lane ln;
   ln.base = 0;
-  ln.stk = reinterpret_cast<uint32_t*>(g_smem) + threadIdx.x;
-  ln.stride = blockDim.x;
+  ln.stk = gstk ? gstk + i : reinterpret_cast<uint32_t*>(g_smem) + threadIdx.x;
+  ln.stride = gstk ? (int)n : (int)blockDim.x;
   Counters c;
   for (int k = 0; k < ST_N; ++k) c.v[k] = 0;
   const srt_ray r = rays[i];

@@ -242,6 +242,11 @@ void CameraParams(const srt_context* c, srt::KParams* kp) {
 
 int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
   if (c->W <= 0 || c->H <= 0) { srt::SetError("Width/Height not set"); return SRT_ERR_STATE; }
+  // sample_kernel packs a pixel as x | local_row << 16 (kernels.hpp refill)
+  if (c->W > 65535 || LocalRows(c, c->H) > 32767) {
+    srt::SetError("Width > 65535 or more than 32767 rows per rank");
+    return SRT_ERR_LIMIT;
+  }
   if (c->show_model && !c->scene_ok) { srt::SetError("showModel set but no scene uploaded"); return SRT_ERR_STATE; }
   if (need_images) {
     if (c->noise_texels != (size_t)c->W * (size_t)c->H) {
@@ -1050,30 +1055,36 @@ int srt_trace_closest(srt_context* c, const srt_ray* rays, uint32_t n, uint32_t*
   kp.bvh_count = c->bvh_count;
   kp.stack_entries = c->stack_entries;
   kp.stats = c->d_stats;
-  srt_ray* d_rays = nullptr;
-  uint32_t* d_hits = nullptr;
-  float* d_t = nullptr;
-  HIP_OK(hipMalloc(&d_rays, sizeof(srt_ray) * n));
-  HIP_OK(hipMalloc(&d_hits, sizeof(uint32_t) * n));
-  HIP_OK(hipMalloc(&d_t, sizeof(float) * n));
-  HIP_OK(hipMemcpyAsync(d_rays, rays, sizeof(srt_ray) * n, hipMemcpyHostToDevice, c->stream));
+  // one 3-dword stack entry per tree level and lane: in LDS while 64 KiB hold a 256- (down to 64-)
+  // lane block's stacks, else in HBM (lane-interleaved; trees deeper than ~85 levels)
+  const size_t entry = 3 * sizeof(uint32_t) * (size_t)kp.stack_entries;
+  int block = 256;
+  while (block > 64 && (size_t)block * entry > 65536) block >>= 1;
+  const bool hbm_stack = (size_t)block * entry > 65536;
+  const size_t lds = hbm_stack ? 0 : (size_t)block * entry;
+  // device buffers, freed on every path
+  struct Buf {
+    void* p = nullptr;
+    ~Buf() { if (p) (void)hipFree(p); }
+  } d_rays, d_hits, d_t, d_stk;
+  HIP_OK(hipMalloc(&d_rays.p, sizeof(srt_ray) * n));
+  HIP_OK(hipMalloc(&d_hits.p, sizeof(uint32_t) * n));
+  HIP_OK(hipMalloc(&d_t.p, sizeof(float) * n));
+  if (hbm_stack) HIP_OK(hipMalloc(&d_stk.p, entry * n));
+  HIP_OK(hipMemcpyAsync(d_rays.p, rays, sizeof(srt_ray) * n, hipMemcpyHostToDevice, c->stream));
   HIP_OK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_N, c->stream));
-  const int block = 256;
-  const size_t lds = (size_t)block * 3 * sizeof(uint32_t) * (size_t)kp.stack_entries;
-  hipLaunchKernelGGL(srt::closest_kernel, dim3((n + block - 1) / block), dim3(block), lds, c->stream, kp, d_rays, n,
-                     d_hits, d_t);
+  hipLaunchKernelGGL(srt::closest_kernel, dim3((n + block - 1) / block), dim3(block), lds, c->stream, kp,
+                     static_cast<const srt_ray*>(d_rays.p), n, static_cast<uint32_t*>(d_hits.p),
+                     static_cast<float*>(d_t.p), static_cast<uint32_t*>(d_stk.p));
   HIP_OK(hipGetLastError());
   unsigned long long s[srt::ST_N];
-  HIP_OK(hipMemcpyAsync(hits, d_hits, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipMemcpyAsync(t_out, d_t, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipMemcpyAsync(hits, d_hits.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipMemcpyAsync(t_out, d_t.p, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipMemcpyAsync(s, c->d_stats, sizeof(s), hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
   c->stats.rays += n;
   c->stats.nodes += s[srt::ST_NODES];
   c->stats.tris += s[srt::ST_TRIS];
-  (void)hipFree(d_rays);
-  (void)hipFree(d_hits);
-  (void)hipFree(d_t);
   return SRT_OK;
 }
 

@@ -1,0 +1,65 @@
+"""Writes profiles/counters.json from a round's rocprofv3 PMC passes (tools/profile_round.sh).
+
+usage: python tools/pmc_roofline.py gpurun_out/r02 [--tag r02]
+
+Each pass ran `python bench.py --steps 1 --warmup 0 --no-cpu-baseline`, so every leg's timed step
+launched its sample_kernel<false, ...> instance exactly once (the counting run is the <true, ...>
+instance).  Per leg and launch:
+  SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU, SQ_LDS_IDX_ACTIVE, SQ_LDS_BANK_CONFLICT, SQ_WAVE_CYCLES,
+  SQ_WAIT_ANY, SQ_BUSY_CYCLES, SQ_INSTS_SALU, GRBM_GUI_ACTIVE  (one SQ pass)
+  hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024  (separate passes; MI355X_MICROARCH.md 'HBM':
+              gfx950 FETCH_SIZE tallies 128-B requests at 64 B, WRITE_SIZE is exact for 16-B stores)
+bench.py divides these by its live kernel time (HIP events) to report the roofs.
+"""
+import csv
+import json
+import pathlib
+import sys
+
+out_dir = pathlib.Path(sys.argv[1])
+tag = sys.argv[sys.argv.index("--tag") + 1] if "--tag" in sys.argv else out_dir.name
+root = pathlib.Path(__file__).resolve().parent.parent
+
+LEGS = {  # kernel instance -> workload name bench.py reports
+    "void srt::sample_kernel<false, true, true, 1024, false>": "rubik_1920x1080_256spp",
+    "void srt::sample_kernel<false, false, true, 256, false>": "synthetic1000000_1920x1080_16spp",
+}
+
+
+def rows(sub):
+    p = out_dir / sub / "run_counter_collection.csv"
+    return list(csv.DictReader(open(p)))
+
+
+def per_launch(sub):
+    """{workload: {counter: value}} of each leg's last dispatch (summed over the dimensions rocprofv3 splits)."""
+    out = {}
+    for leg_kernel, wl in LEGS.items():
+        rs = [r for r in rows(sub) if r["Kernel_Name"].startswith(leg_kernel)]
+        if not rs:
+            continue
+        last = max(int(r["Dispatch_Id"]) for r in rs)
+        agg = {}
+        for r in rs:
+            if int(r["Dispatch_Id"]) == last:
+                agg[r["Counter_Name"]] = agg.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        out[wl] = agg
+    return out
+
+
+sq, fetch, write = per_launch("pmc_sq"), per_launch("pmc_fetch"), per_launch("pmc_write")
+p = root / "profiles" / "counters.json"
+data = json.loads(p.read_text()) if p.exists() else {}
+for wl in sq:
+    d = dict(sq[wl])
+    d["FETCH_SIZE"] = fetch[wl]["FETCH_SIZE"]
+    d["WRITE_SIZE"] = write[wl]["WRITE_SIZE"]
+    d["hbm_bytes"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
+    d["source"] = (f"rocprofv3 --pmc passes ({tag}): SQ counters + GRBM_GUI_ACTIVE, FETCH_SIZE, WRITE_SIZE; "
+                   f"python bench.py --steps 1 --warmup 0 --no-cpu-baseline; per launch of the timed step")
+    data[wl] = d
+    lane = d["SQ_THREAD_CYCLES_VALU"] / (64 * d["SQ_INSTS_VALU"])
+    print(f"{wl}: VALU {d['SQ_INSTS_VALU']:.4g} insts, lane util {lane:.3f}, LDS active {d['SQ_LDS_IDX_ACTIVE']:.4g}, "
+          f"conflict {d['SQ_LDS_BANK_CONFLICT'] / max(d['SQ_LDS_IDX_ACTIVE'], 1):.3f}, HBM {d['hbm_bytes'] / 1e9:.2f} GB, "
+          f"wait {d['SQ_WAIT_ANY'] / d['SQ_WAVE_CYCLES']:.3f}")
+p.write_text(json.dumps(data, indent=1) + "\n")
