@@ -29,6 +29,9 @@ namespace srt {
 struct vec3 {
   float x = 0.f, y = 0.f, z = 0.f;
 };
+struct vec2 {
+  float x = 0.f, y = 0.f;
+};
 
 inline void check(int code, const char* what) {
   if (code != SRT_OK) throw std::runtime_error(std::string(what) + ": " + srt_last_error());
@@ -246,35 +249,34 @@ inline srt_light PointLight(const vec3& position, const vec3& color, float inten
   return l;
 }
 
-// Camera basis vectors as uploaded by src/main.cpp:672-675
+// RayTracer::Camera (src/raytracer/camera.cpp, include/raytracer/camera.h) over srt_camera:
+// the basis vectors src/main.cpp:672-675 uploads, Move*, Rotate, MoveAndRotate, Reset.
 class Camera {
  public:
-  explicit Camera(bool show_model) : show_model_(show_model) { Reset(); }
-  void Reset() {
-    float o[3], f[3], u[3], r[3];
-    check(srt_camera_reset(show_model_ ? 1 : 0, o, f, u, r), "Camera::Reset");
-    position_ = {o[0], o[1], o[2]}; front_ = {f[0], f[1], f[2]}; up_ = {u[0], u[1], u[2]}; right_ = {r[0], r[1], r[2]};
-    yaw_ = -90.0f;
-    pitch_ = 0.0f;
-  }
+  explicit Camera(bool show_model) { check(srt_camera_init(&s_, show_model ? 1 : 0), "Camera"); }
+  void Reset() { check(srt_camera_state_reset(&s_), "Camera::Reset"); }
   void Rotate(float yaw_offset, float pitch_offset) {
-    yaw_ += yaw_offset;
-    pitch_ += pitch_offset;
-    if (pitch_ > 89.0f) pitch_ = 89.0f;
-    if (pitch_ < -89.0f) pitch_ = -89.0f;
-    float f[3], u[3], r[3];
-    check(srt_camera_basis(yaw_, pitch_, f, u, r), "Camera::Rotate");
-    front_ = {f[0], f[1], f[2]}; up_ = {u[0], u[1], u[2]}; right_ = {r[0], r[1], r[2]};
+    check(srt_camera_rotate(&s_, yaw_offset, pitch_offset), "Camera::Rotate");
   }
-  vec3 getOrigin() const { return position_; }
-  vec3 getForward() const { return front_; }
-  vec3 getUpVector() const { return up_; }
-  vec3 getRightVector() const { return right_; }
+  void MoveForward(float d) { check(srt_camera_move(&s_, SRT_MOVE_FORWARD, d), "Camera::MoveForward"); }
+  void MoveBackward(float d) { check(srt_camera_move(&s_, SRT_MOVE_BACKWARD, d), "Camera::MoveBackward"); }
+  void MoveLeft(float d) { check(srt_camera_move(&s_, SRT_MOVE_LEFT, d), "Camera::MoveLeft"); }
+  void MoveRight(float d) { check(srt_camera_move(&s_, SRT_MOVE_RIGHT, d), "Camera::MoveRight"); }
+  void MoveUp(float d) { check(srt_camera_move(&s_, SRT_MOVE_UP, d), "Camera::MoveUp"); }
+  void MoveDown(float d) { check(srt_camera_move(&s_, SRT_MOVE_DOWN, d), "Camera::MoveDown"); }
+  void MoveAndRotate(float delta_time, const vec3& movement_delta, const vec2& rotation_delta, float speed) {
+    const float m[3] = {movement_delta.x, movement_delta.y, movement_delta.z};
+    const float r[2] = {rotation_delta.x, rotation_delta.y};
+    check(srt_camera_move_and_rotate(&s_, delta_time, m, r, speed), "Camera::MoveAndRotate");
+  }
+  vec3 getOrigin() const { return {s_.position[0], s_.position[1], s_.position[2]}; }
+  vec3 getForward() const { return {s_.front[0], s_.front[1], s_.front[2]}; }
+  vec3 getUpVector() const { return {s_.up[0], s_.up[1], s_.up[2]}; }
+  vec3 getRightVector() const { return {s_.right[0], s_.right[1], s_.right[2]}; }
+  srt_camera* state() { return &s_; }
 
  private:
-  bool show_model_;
-  vec3 position_, front_, up_, right_;
-  float yaw_ = -90.0f, pitch_ = 0.0f;
+  srt_camera s_{};
 };
 
 }  // namespace RayTracer

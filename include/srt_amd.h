@@ -254,6 +254,41 @@ int srt_camera_reset(int show_model, float origin[3], float front[3], float up[3
 /* Camera::Rotate(yaw, pitch) basis from angles in degrees (camera.cpp:107-136). */
 int srt_camera_basis(float yaw_deg, float pitch_deg, float front[3], float up[3], float right[3]);
 
+/* ---- interactive mode ---------------------------------
+ * RayTracer::Camera's state (include/raytracer/camera.h:30-96).  frame_counter
+ * is MoveAndRotate's function-static counter (camera.cpp:175), kept per camera
+ * (the reference app has one camera, so the two agree). */
+typedef struct {
+  float position[3], front[3], up[3], right[3];
+  float yaw, pitch;          /* degrees */
+  int32_t show_model;
+  int32_t frame_counter;
+} srt_camera;
+enum { SRT_MOVE_FORWARD = 0, SRT_MOVE_BACKWARD, SRT_MOVE_LEFT, SRT_MOVE_RIGHT, SRT_MOVE_UP, SRT_MOVE_DOWN };
+/* Camera(settings) + Initialize + Reset as src/main.cpp:439-441 does; frame_counter = 0. */
+int srt_camera_init(srt_camera* cam, int show_model);
+/* Camera::Reset (camera.cpp:187-212); keeps frame_counter, as the static does. */
+int srt_camera_state_reset(srt_camera* cam);
+/* Camera::MoveForward .. MoveDown (camera.cpp:71-105); direction = SRT_MOVE_*. */
+int srt_camera_move(srt_camera* cam, int direction, float delta);
+/* Camera::Rotate (camera.cpp:107-118): pitch clamped to +-89, yaw unwrapped. */
+int srt_camera_rotate(srt_camera* cam, float yaw_offset, float pitch_offset);
+/* Camera::MoveAndRotate (camera.cpp:138-185).  SRT_ERR_INVALID (camera
+ * unchanged) where the reference's yaw wrap loop would never end (an infinite
+ * yaw, or one whose ulp exceeds 720). */
+int srt_camera_move_and_rotate(srt_camera* cam, float delta_time, const float movement_delta[3],
+                               const float rotation_delta[2], float movement_speed);
+/* The frame loop's host side, src/main.cpp:622-659: resetAccumBuffer is set
+ * (and *accum_frames zeroed) on any input -- |movement| > 1e-4, |rotation| >
+ * 1e-4 or the left mouse button held -- or when the input handler's reset flag
+ * is up (the flag is then cleared, input_handler.cpp:160-168); the camera moves
+ * with MoveAndRotate(delta_time, ..., 1.0); *accum_frames is incremented.  The
+ * caller then sets resetAccumBuffer = *reset_buffer, accumFrames and the camera
+ * uniforms and dispatches, as main.cpp:668-706 does. */
+int srt_progressive_frame(srt_camera* cam, const float movement_delta[3], const float rotation_delta[2],
+                          int mouse_left, int32_t* should_reset_buffer, float delta_time, int32_t* accum_frames,
+                          int32_t* reset_buffer);
+
 #ifdef __cplusplus
 }
 #endif

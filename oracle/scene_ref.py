@@ -9,7 +9,9 @@ noise.cpp, camera.cpp) so tests can check them array-for-array, bit-for-bit:
   (src/asset_utils/model_loader.cpp:35-365);
 * ``BVH<GPU::Triangle>`` (include/intersection_utils/bvh.h:40-148);
 * ``UploadModelDataToGPU``'s flattening (src/asset_utils/gpu_loader.cpp:63-133);
-* ``Camera::UpdateCameraVectors`` (src/raytracer/camera.cpp:120-136).
+* ``Camera::UpdateCameraVectors`` (src/raytracer/camera.cpp:120-136), the camera's
+  interactive state (``Move*``, ``Rotate``, ``MoveAndRotate``, ``Reset``;
+  camera.cpp:71-212) and the frame loop's reset schedule (src/main.cpp:622-659).
 
 All float arithmetic is numpy float32 scalar arithmetic in source order.
 """
@@ -316,3 +318,88 @@ def camera_basis(yaw: float, pitch: float):
     right = _normalize(_cross(front, (F(0), F(1), F(0))))
     up = _normalize(_cross(right, front))
     return front, up, right
+
+
+def _f3(v):
+    return tuple(F(c) for c in v)
+
+
+class CameraRef:
+    """RayTracer::Camera's interactive state (include/raytracer/camera.h:30-96, src/raytracer/camera.cpp).
+    `frame_counter` is MoveAndRotate's function-static counter (camera.cpp:175)."""
+
+    def __init__(self, show_model: bool):
+        # camera.h:34-37 with default CameraSettings, then Initialize + Reset (src/main.cpp:439-441)
+        self.show_model = bool(show_model)
+        self.position = (F(0), F(0), F(0))
+        self.front = _normalize((F(0), F(0), F(-1)))
+        self.up = (F(0), F(1), F(0))
+        self.right = _normalize(_cross(self.front, self.up))
+        self.yaw, self.pitch = F(-90.0), F(0.0)
+        self.frame_counter = 0
+        self._update()
+        self.reset()
+
+    def _update(self):  # UpdateCameraVectors (camera.cpp:120-136)
+        self.front, self.up, self.right = camera_basis(self.yaw, self.pitch)
+
+    def reset(self):  # camera.cpp:187-212
+        self.position = (F(0), F(9), F(40)) if self.show_model else (F(0), F(1), F(4))
+        self.yaw, self.pitch = F(-90.0), F(0.0)
+        self._update()
+
+    def move(self, direction: int, delta: float):  # camera.cpp:71-105: forward, backward, left, right, up, down
+        d = F(delta)
+        axis = (self.front, self.front, self.right, self.right, self.up, self.up)[direction]
+        sign = (1, -1, -1, 1, 1, -1)[direction]
+        if sign > 0:
+            self.position = tuple(p + a * d for p, a in zip(self.position, axis))
+        else:
+            self.position = tuple(p - a * d for p, a in zip(self.position, axis))
+        self._update()
+
+    def rotate(self, yaw_off: float, pitch_off: float):  # camera.cpp:107-118
+        self.yaw = self.yaw + F(yaw_off)
+        self.pitch = self.pitch + F(pitch_off)
+        if self.pitch > F(89.0):
+            self.pitch = F(89.0)
+        if self.pitch < F(-89.0):
+            self.pitch = F(-89.0)
+        self._update()
+
+    def move_and_rotate(self, dt: float, move, rot, speed: float):  # camera.cpp:138-185
+        mv, rt = _f3(move), (F(rot[0]), F(rot[1]))
+        if abs(rt[0]) > F(0.0001) or abs(rt[1]) > F(0.0001):
+            self.yaw = self.yaw + rt[0]
+            p = self.pitch + rt[1]
+            p = F(-89.0) if p < F(-89.0) else p       # glm::max(x, lo) = x < lo ? lo : x
+            self.pitch = F(89.0) if F(89.0) < p else p  # glm::min(x, hi) = hi < x ? hi : x
+            while self.yaw > F(180.0):
+                self.yaw = self.yaw - F(360.0)
+            while self.yaw < F(-180.0):
+                self.yaw = self.yaw + F(360.0)
+            self._update()
+        if np.sqrt(mv[0] * mv[0] + mv[1] * mv[1] + mv[2] * mv[2]) > F(0.0001):
+            s = F(speed) * F(dt)
+            for axis, k in ((self.front, mv[2]), (self.right, mv[0]), (self.up, mv[1])):
+                self.position = tuple(p + (a * k) * s for p, a in zip(self.position, axis))
+        self.frame_counter += 1
+        if self.frame_counter % 120 == 0:
+            self.front = _normalize(self.front)
+            self.right = _normalize(_cross(self.front, (F(0), F(1), F(0))))
+            self.up = _normalize(_cross(self.right, self.front))
+
+
+def progressive_frame_ref(cam: CameraRef, move, rot, mouse_left: bool, should_reset: bool, dt: float,
+                          accum_frames: int):
+    """src/main.cpp:622-659: returns (accumFrames, resetAccumBuffer, handler flag after the frame)."""
+    mv = _f3(move)
+    rt = (F(rot[0]), F(rot[1]))
+    reset = False
+    if (np.sqrt(mv[0] * mv[0] + mv[1] * mv[1] + mv[2] * mv[2]) > F(0.0001)
+            or np.sqrt(rt[0] * rt[0] + rt[1] * rt[1]) > F(0.0001) or mouse_left):
+        reset, accum_frames = True, 0
+    if should_reset:
+        reset, accum_frames, should_reset = True, 0, False
+    cam.move_and_rotate(dt, mv, rt, 1.0)
+    return accum_frames + 1, reset, should_reset

@@ -254,4 +254,97 @@ int srt_camera_basis(float yaw_deg, float pitch_deg, float front[3], float up[3]
   return SRT_OK;
 }
 
+namespace {
+void ToState(const srt_camera* c, srt::CameraState* s) {
+  s->position = srt::Vec3(c->position[0], c->position[1], c->position[2]);
+  s->front = srt::Vec3(c->front[0], c->front[1], c->front[2]);
+  s->up = srt::Vec3(c->up[0], c->up[1], c->up[2]);
+  s->right = srt::Vec3(c->right[0], c->right[1], c->right[2]);
+  s->yaw = c->yaw;
+  s->pitch = c->pitch;
+  s->show_model = c->show_model != 0;
+  s->frame_counter = c->frame_counter;
+}
+void FromState(const srt::CameraState& s, srt_camera* c) {
+  const srt::Vec3* v[4] = {&s.position, &s.front, &s.up, &s.right};
+  float* d[4] = {c->position, c->front, c->up, c->right};
+  for (int i = 0; i < 4; ++i) { d[i][0] = v[i]->x; d[i][1] = v[i]->y; d[i][2] = v[i]->z; }
+  c->yaw = s.yaw;
+  c->pitch = s.pitch;
+  c->show_model = s.show_model ? 1 : 0;
+  c->frame_counter = s.frame_counter;
+}
+}  // namespace
+
+int srt_camera_init(srt_camera* cam, int show_model) {
+  if (!cam) return SRT_ERR_INVALID;
+  srt::CameraState s;
+  s.Construct(show_model != 0);
+  FromState(s, cam);
+  return SRT_OK;
+}
+
+int srt_camera_state_reset(srt_camera* cam) {
+  if (!cam) return SRT_ERR_INVALID;
+  srt::CameraState s;
+  ToState(cam, &s);
+  s.Reset();
+  FromState(s, cam);
+  return SRT_OK;
+}
+
+int srt_camera_move(srt_camera* cam, int direction, float delta) {
+  if (!cam || direction < SRT_MOVE_FORWARD || direction > SRT_MOVE_DOWN) return SRT_ERR_INVALID;
+  srt::CameraState s;
+  ToState(cam, &s);
+  s.Move(static_cast<srt::CameraMove>(direction), delta);
+  FromState(s, cam);
+  return SRT_OK;
+}
+
+int srt_camera_rotate(srt_camera* cam, float yaw_offset, float pitch_offset) {
+  if (!cam) return SRT_ERR_INVALID;
+  srt::CameraState s;
+  ToState(cam, &s);
+  s.Rotate(yaw_offset, pitch_offset);
+  FromState(s, cam);
+  return SRT_OK;
+}
+
+int srt_camera_move_and_rotate(srt_camera* cam, float delta_time, const float movement_delta[3],
+                               const float rotation_delta[2], float movement_speed) {
+  if (!cam || !movement_delta || !rotation_delta) return SRT_ERR_INVALID;
+  srt::CameraState s;
+  ToState(cam, &s);
+  const srt::Vec3 mv(movement_delta[0], movement_delta[1], movement_delta[2]);
+  if (!s.MoveAndRotate(delta_time, mv, rotation_delta[0], rotation_delta[1], movement_speed)) {
+    srt::SetError("srt_camera_move_and_rotate: yaw cannot be wrapped into [-180, 180]");
+    return SRT_ERR_INVALID;
+  }
+  FromState(s, cam);
+  return SRT_OK;
+}
+
+int srt_progressive_frame(srt_camera* cam, const float movement_delta[3], const float rotation_delta[2],
+                          int mouse_left, int32_t* should_reset_buffer, float delta_time, int32_t* accum_frames,
+                          int32_t* reset_buffer) {
+  if (!cam || !movement_delta || !rotation_delta || !should_reset_buffer || !accum_frames || !reset_buffer)
+    return SRT_ERR_INVALID;
+  srt::CameraState s;
+  ToState(cam, &s);
+  const srt::Vec3 mv(movement_delta[0], movement_delta[1], movement_delta[2]);
+  bool flag = *should_reset_buffer != 0, reset = false;
+  int32_t frames = *accum_frames;
+  if (!srt::ProgressiveFrame(&s, mv, rotation_delta[0], rotation_delta[1], mouse_left != 0, &flag, delta_time,
+                             &frames, &reset)) {
+    srt::SetError("srt_progressive_frame: yaw cannot be wrapped into [-180, 180]");
+    return SRT_ERR_INVALID;
+  }
+  FromState(s, cam);
+  *should_reset_buffer = flag ? 1 : 0;
+  *accum_frames = frames;
+  *reset_buffer = reset ? 1 : 0;
+  return SRT_OK;
+}
+
 }  // extern "C"

@@ -103,6 +103,28 @@ void GenerateNoise(uint32_t texels, bool gcc_order, float* noise, float* noise_u
 void CameraReset(bool show_model, Vec3* origin, Vec3* front, Vec3* up, Vec3* right);
 void CameraBasis(float yaw, float pitch, Vec3* front, Vec3* up, Vec3* right);
 
+enum class CameraMove { kForward = 0, kBackward, kLeft, kRight, kUp, kDown };
+
+// RayTracer::Camera's interactive state (include/raytracer/camera.h:30-96).
+struct CameraState {
+  Vec3 position, front, up, right;
+  float yaw = -90.0f, pitch = 0.0f;
+  bool show_model = true;
+  int32_t frame_counter = 0;  // MoveAndRotate's static counter (camera.cpp:175)
+
+  void Construct(bool model);  // constructor + Initialize + Reset (src/main.cpp:439-441)
+  void Reset();
+  void UpdateVectors();
+  void Move(CameraMove dir, float delta);
+  void Rotate(float yaw_offset, float pitch_offset);
+  // false (state unchanged) where the reference's yaw wrap would never end
+  bool MoveAndRotate(float delta_time, const Vec3& move, float rot_x, float rot_y, float speed);
+};
+
+// One frame of src/main.cpp:622-659: reset decision, MoveAndRotate, accumFrames.
+bool ProgressiveFrame(CameraState* cam, const Vec3& move, float rot_x, float rot_y, bool mouse_left,
+                      bool* should_reset_buffer, float delta_time, int32_t* accum_frames, bool* reset_buffer);
+
 void SetError(const std::string& msg);
 
 }  // namespace srt

@@ -29,7 +29,7 @@ from ._lib import SrtError, check, lib
 
 __all__ = [
     "Compute", "Model", "Scene", "LoadObject", "load_obj", "model_from_triangles", "UploadModelDataToGPU",
-    "UpdateModelMatrix", "Camera", "PointLight", "generate_noise", "glibc_rand", "SrtError",
+    "UpdateModelMatrix", "Camera", "InputState", "progressive_frame", "PointLight", "generate_noise", "glibc_rand", "SrtError",
     "NODE_DTYPE", "BVH_DTYPE", "MAT_DTYPE", "TRI_DTYPE", "VERT_DTYPE", "LIGHT_DTYPE", "RAY_DTYPE",
     "MODEL_LIGHTS", "SPHERE_LIGHTS", "REFERENCE_OBJECTS",
 ]
@@ -92,25 +92,80 @@ def lights_array(lights: Iterable[PointLight]) -> np.ndarray:
 
 
 class Camera:
-    """Camera basis as RayTracer::Camera produces it (src/raytracer/camera.cpp:120-212)."""
+    """RayTracer::Camera (src/raytracer/camera.cpp, include/raytracer/camera.h) over the C ABI's srt_camera
+    state: construction + Initialize + Reset as src/main.cpp:439-441, Move*, Rotate, MoveAndRotate."""
+
+    FORWARD, BACKWARD, LEFT, RIGHT, UP, DOWN = range(6)
 
     def __init__(self, show_model: bool = True):
         self.show_model = bool(show_model)
-        self.Reset()
+        self.state = _lib.CameraState()
+        check(lib().srt_camera_init(C.byref(self.state), int(self.show_model)), "srt_camera_init")
 
     def Reset(self):
-        o, f, u, r = (np.zeros(3, np.float32) for _ in range(4))
-        check(lib().srt_camera_reset(int(self.show_model), _ptr(o), _ptr(f), _ptr(u), _ptr(r)), "srt_camera_reset")
-        self.position, self.front, self.up, self.right = o, f, u, r
-        self.yaw, self.pitch = -90.0, 0.0
+        check(lib().srt_camera_state_reset(C.byref(self.state)), "srt_camera_state_reset")
 
     def Rotate(self, yaw_offset: float, pitch_offset: float):
-        self.yaw += yaw_offset
-        self.pitch = min(max(self.pitch + pitch_offset, -89.0), 89.0)
-        f, u, r = (np.zeros(3, np.float32) for _ in range(3))
-        check(lib().srt_camera_basis(C.c_float(self.yaw), C.c_float(self.pitch), _ptr(f), _ptr(u), _ptr(r)),
-              "srt_camera_basis")
-        self.front, self.up, self.right = f, u, r
+        check(lib().srt_camera_rotate(C.byref(self.state), C.c_float(yaw_offset), C.c_float(pitch_offset)),
+              "srt_camera_rotate")
+
+    def _move(self, direction: int, delta: float):
+        check(lib().srt_camera_move(C.byref(self.state), direction, C.c_float(delta)), "srt_camera_move")
+
+    def MoveForward(self, delta: float):
+        self._move(self.FORWARD, delta)
+
+    def MoveBackward(self, delta: float):
+        self._move(self.BACKWARD, delta)
+
+    def MoveLeft(self, delta: float):
+        self._move(self.LEFT, delta)
+
+    def MoveRight(self, delta: float):
+        self._move(self.RIGHT, delta)
+
+    def MoveUp(self, delta: float):
+        self._move(self.UP, delta)
+
+    def MoveDown(self, delta: float):
+        self._move(self.DOWN, delta)
+
+    def MoveAndRotate(self, delta_time: float, movement_delta, rotation_delta, movement_speed: float):
+        m = np.asarray(movement_delta, np.float32).reshape(3)
+        r = np.asarray(rotation_delta, np.float32).reshape(2)
+        check(lib().srt_camera_move_and_rotate(C.byref(self.state), C.c_float(delta_time), _ptr(m), _ptr(r),
+                                               C.c_float(movement_speed)), "srt_camera_move_and_rotate")
+
+    def _v(self, name):
+        return np.array(getattr(self.state, name)[:], np.float32)
+
+    @property
+    def position(self):
+        return self._v("position")
+
+    @position.setter
+    def position(self, v):
+        self.state.position[:] = [float(x) for x in np.asarray(v, np.float32).reshape(3)]
+
+    @property
+    def front(self):
+        return self._v("front")
+
+    @property
+    def up(self):
+        return self._v("up")
+
+    @property
+    def right(self):
+        return self._v("right")
+
+    @property
+    def yaw(self):
+        return np.float32(self.state.yaw)
+
+    @property
+    def pitch(self):
+        return np.float32(self.state.pitch)
 
     def getOrigin(self):
         return self.position
@@ -123,6 +178,32 @@ class Camera:
 
     def getRightVector(self):
         return self.right
+
+
+@dataclass
+class InputState:
+    """What the frame loop reads from InputHandler each frame (include/input_handler.h): the movement and
+    rotation deltas, the left mouse button, and the handler's shouldResetBuffer flag.  The app starts with the
+    flag up (EnableMouseCapture(false), src/main.cpp:451, input_handler.cpp:172)."""
+    movement_delta: Sequence[float] = (0.0, 0.0, 0.0)
+    rotation_delta: Sequence[float] = (0.0, 0.0)
+    mouse_left: bool = False
+    should_reset_buffer: bool = True
+
+
+def progressive_frame(camera: Camera, inp: InputState, delta_time: float, accum_frames: int) -> tuple[int, bool]:
+    """One frame of src/main.cpp:622-659: returns (accumFrames, resetAccumBuffer) to upload; moves the camera
+    and clears inp.should_reset_buffer as the loop does."""
+    m = np.asarray(inp.movement_delta, np.float32).reshape(3)
+    r = np.asarray(inp.rotation_delta, np.float32).reshape(2)
+    flag = C.c_int32(int(bool(inp.should_reset_buffer)))
+    af = C.c_int32(int(accum_frames))
+    reset = C.c_int32(0)
+    check(lib().srt_progressive_frame(C.byref(camera.state), _ptr(m), _ptr(r), int(bool(inp.mouse_left)),
+                                      C.byref(flag), C.c_float(delta_time), C.byref(af), C.byref(reset)),
+          "srt_progressive_frame")
+    inp.should_reset_buffer = bool(flag.value)
+    return int(af.value), bool(reset.value)
 
 
 def glibc_rand(n: int) -> np.ndarray:

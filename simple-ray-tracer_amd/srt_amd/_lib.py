@@ -55,6 +55,13 @@ class Light(C.Structure):
                 ("pad1", C.c_float)]
 
 
+class CameraState(C.Structure):
+    """srt_camera: RayTracer::Camera's interactive state (include/raytracer/camera.h:30-96)."""
+    _fields_ = [("position", C.c_float * 3), ("front", C.c_float * 3), ("up", C.c_float * 3),
+                ("right", C.c_float * 3), ("yaw", C.c_float), ("pitch", C.c_float), ("show_model", C.c_int32),
+                ("frame_counter", C.c_int32)]
+
+
 class Ray(C.Structure):
     _fields_ = [("origin", C.c_float * 3), ("pad0", C.c_float), ("direction", C.c_float * 3),
                 ("intersection_distance", C.c_float)]
@@ -132,6 +139,13 @@ _SIGS = {
     "srt_glibc_rand": (C.c_int, [C.c_uint32, P]),
     "srt_camera_reset": (C.c_int, [C.c_int, P, P, P, P]),
     "srt_camera_basis": (C.c_int, [C.c_float, C.c_float, P, P, P]),
+    "srt_camera_init": (C.c_int, [C.POINTER(CameraState), C.c_int]),
+    "srt_camera_state_reset": (C.c_int, [C.POINTER(CameraState)]),
+    "srt_camera_move": (C.c_int, [C.POINTER(CameraState), C.c_int, C.c_float]),
+    "srt_camera_rotate": (C.c_int, [C.POINTER(CameraState), C.c_float, C.c_float]),
+    "srt_camera_move_and_rotate": (C.c_int, [C.POINTER(CameraState), C.c_float, P, P, C.c_float]),
+    "srt_progressive_frame": (C.c_int, [C.POINTER(CameraState), P, P, C.c_int, C.POINTER(C.c_int32), C.c_float,
+                                        C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

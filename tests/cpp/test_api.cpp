@@ -74,10 +74,22 @@ int main(int argc, char** argv) {
   Common::GenerateNoise(W, H, &noise, &noise_u);
   rt.BindNoise(noise, noise_u);
   rt.BindLights(lights);
+  // A scripted input sequence through the loop's host side (main.cpp:622-659): frames 0-2 idle (frame 0
+  // resets: EnableMouseCapture(false) raised the handler's flag), frame 3 holds W with a mouse drag
+  // (reset, MoveAndRotate moves and turns the camera), frames 4-6 idle: the final image is the reset
+  // frame + 3 sampled frames from the moved camera.
   int accumFrames = 0;
-  for (int frame = 0; frame < 4; ++frame) {
-    const bool resetBuffer = frame == 0;  // EnableMouseCapture(false) sets the reset flag
-    accumFrames++;
+  int32_t shouldResetBuffer = 1;
+  for (int frame = 0; frame < 7; ++frame) {
+    const bool drag = frame == 3;
+    const float move[3] = {0.0f, 0.0f, drag ? 1.0f : 0.0f};
+    const float rot[2] = {drag ? 10.0f : 0.0f, drag ? -5.0f : 0.0f};
+    int32_t reset = 0;
+    check(srt_progressive_frame(camera.state(), move, rot, drag ? 1 : 0, &shouldResetBuffer, 0.5f, &accumFrames,
+                                &reset),
+          "srt_progressive_frame");
+    const bool resetBuffer = reset != 0;
+    if (resetBuffer != (frame == 0 || frame == 3)) return fail("reset schedule");
     rt.SetBool("resetAccumBuffer", resetBuffer);
     rt.SetVec3("cameraOrigin", camera.getOrigin());
     rt.SetVec3("cameraDirection", camera.getForward());
@@ -92,6 +104,7 @@ int main(int argc, char** argv) {
     rt.Dispatch(W / 8, H / 8, 1);
     rt.Finish();
   }
+  if (accumFrames != 4) return fail("accumFrames after the script");
   const auto out = rt.ReadOutput();
   const auto acc = rt.ReadAccum();
   if (!out_prefix.empty()) {

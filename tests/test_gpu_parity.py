@@ -302,7 +302,8 @@ def test_full_frame_rows_and_determinism(rubik):
 
 def test_cpp_api_program(rubik, tmp_path):
     """The C++ mirror API running the reference's integration test + main loop (tests/cpp/test_api.cpp);
-    the loop's frame (reset + 3 sampled frames of Rubik at 64x48) is checked against the oracle."""
+    the loop's frame (a scripted camera move resets it: reset + 3 sampled frames of Rubik at 64x48 from the
+    moved camera) is checked against the oracle."""
     exe = ROOT / "tests" / "cpp" / "_build" / "test_api"
     exe.parent.mkdir(exist_ok=True)
     subprocess.run(["g++", "-std=c++17", "-O1", "-I", str(ROOT / "include"), str(ROOT / "tests/cpp/test_api.cpp"),
@@ -316,7 +317,16 @@ def test_cpp_api_program(rubik, tmp_path):
     assert res.returncode == 0 and res.stdout.startswith("OK"), res.stdout + res.stderr
     acc = np.fromfile(tmp_path / "loop.accum", np.float32).reshape(48, 64, 4)
     out = np.fromfile(tmp_path / "loop.rgba8", np.uint8).reshape(48, 64, 4)
-    want_acc, want_out, _ = oracle_render(R.make_setup(64, 48, show_model=True, models=[rubik]), 3)
+    from oracle import scene_ref as REF
+
+    setup = R.make_setup(64, 48, show_model=True, models=[rubik])
+    cam = REF.CameraRef(True)  # test_api.cpp's script: 3 idle frames, then W + a (10, -5) drag for 0.5 s
+    for frame in range(4):
+        drag = frame == 3
+        REF.progressive_frame_ref(cam, (0.0, 0.0, 1.0 if drag else 0.0), (10.0, -5.0) if drag else (0.0, 0.0),
+                                  drag, frame == 0, 0.5, 0)
+    setup.camera = cam
+    want_acc, want_out, _ = oracle_render(setup, 3)
     assert bits_equal(acc, want_acc).all()
     assert (out == want_out).all()
 
