@@ -19,6 +19,8 @@ from __future__ import annotations
 
 import math
 import pathlib
+import re
+from fractions import Fraction
 
 import numpy as np
 
@@ -95,14 +97,81 @@ def _trim(line: str) -> str:
     return line.strip(" \n\r\t")
 
 
-def _floats(tokens, n):
-    out = []
-    for t in tokens[:n]:
-        try:
-            out.append(F(float(t)))
-        except ValueError:
-            break
-    return out
+_WS = " \t\n\r\f\v"
+_DEC = re.compile(r"^[+-]?(\d+\.?\d*|\.\d+)([eE][+-]?\d+)?$")
+_FLT_MAX = F(np.finfo(np.float32).max)
+
+
+def _round_f32(text: str) -> np.float32:
+    """strtof: the decimal `text` rounded once, to nearest-even float32 (±inf past the largest float)."""
+    q = Fraction(text)
+    neg = text.lstrip().startswith("-")
+    a = abs(q)
+    if a >= Fraction(2 ** 103) * (2 ** 25 - 1):  # (2 - 2^-24) * 2^127: rounds to inf
+        r = F(np.inf)
+    elif a == 0:
+        r = F(0.0)
+    else:
+        c = np.float32(float(a))  # within one ulp of the answer (double rounding)
+        with np.errstate(over="ignore"):
+            cands = [c, np.nextafter(c, F(0)), np.nextafter(c, F(np.inf))]
+        cands = [x for x in cands if np.isfinite(x)]
+
+        def key(x):
+            return (abs(Fraction(float(x)) - a), int(np.array(x).view(np.uint32)) & 1)
+
+        r = min(cands, key=key)
+    return -r if neg else r
+
+
+def istream_floats(rest: str, n: int):
+    """`ls >> f1 >> ... >> fn` on an istringstream over `rest` (libstdc++ num_get::_M_extract_float under the
+    "C" locale, model_loader.cpp:59,67,237,251,256): each extraction skips whitespace (none left: failbit, the
+    float untouched), takes the longest prefix of [sign] digits [. digits] [e [sign] digits] (a decimal point
+    once, an exponent only after a mantissa digit), and converts it with strtof; a prefix strtof does not
+    consume whole reads 0.0 and one past the float range +-FLT_MAX, both with failbit.  After a failure
+    nothing more is read.  Returns (stream ok, [value or None if untouched] * n).  tests/cpp/istream_probe.cpp
+    pins this against the library."""
+    vals = [None] * n
+    pos, L = 0, len(rest)
+    for i in range(n):
+        while pos < L and rest[pos] in _WS:
+            pos += 1
+        if pos >= L:
+            return False, vals
+        j = pos
+        if rest[j] in "+-":
+            j += 1
+        mant = dot = False
+        while j < L:
+            ch = rest[j]
+            if "0" <= ch <= "9":
+                mant = True
+            elif ch == "." and not dot:
+                dot = True
+            else:
+                break
+            j += 1
+        if j < L and rest[j] in "eE" and mant:
+            j += 1
+            if j < L and rest[j] in "+-":
+                j += 1
+            while j < L and "0" <= rest[j] <= "9":
+                j += 1
+        tok, pos = rest[pos:j], j
+        if not _DEC.match(tok):
+            vals[i] = F(0.0)
+            return False, vals
+        v = _round_f32(tok)
+        if np.isinf(v):
+            vals[i] = _FLT_MAX if v > 0 else -_FLT_MAX
+            return False, vals
+        vals[i] = v
+    return True, vals
+
+
+def _rest(line: str, prefix: str) -> str:
+    return line[len(prefix):]
 
 
 def parse_obj(path):
@@ -116,8 +185,8 @@ def parse_obj(path):
         tok = line.split()
         prefix = tok[0]
         if prefix == "v":
-            f = _floats(tok[1:], 3)
-            if len(f) == 3:
+            ok, f = istream_floats(_rest(line, prefix), 3)
+            if ok:
                 verts.append(tuple(f))
         elif prefix == "f":
             vi = []
@@ -169,14 +238,12 @@ def parse_mtl(path, names, mats):
         m = mats[current]
         if prefix == "map_Kd":
             m["tex"] = tok[1] if len(tok) > 1 else ""
-        elif prefix in ("Kd", "Ks"):
-            f = _floats(tok[1:], 3)
-            while len(f) < 3:
-                f.append(F(0))
-            m[prefix] = tuple(f)
+        elif prefix in ("Kd", "Ks"):  # model_loader.cpp:234-252 (unread components: 0, see scene.cpp)
+            _, f = istream_floats(_rest(line, prefix), 3)
+            m[prefix] = tuple(F(0) if x is None else x for x in f)
         elif prefix == "Ns":
-            f = _floats(tok[1:], 1)
-            m["Ns"] = f[0] if f else F(0)
+            _, f = istream_floats(_rest(line, prefix), 1)
+            m["Ns"] = F(0) if f[0] is None else f[0]
 
 
 def load_obj(obj_path):

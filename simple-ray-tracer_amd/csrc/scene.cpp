@@ -36,19 +36,6 @@ void Trim(std::string* line) {
   line->erase(last == std::string::npos ? 0 : last + 1);
 }
 
-// istream >> float: leading whitespace skipped, longest valid prefix parsed.
-bool ReadFloat(std::istringstream& ls, float* out) {
-  std::string tok;
-  if (!(ls >> tok)) return false;
-  const char* s = tok.c_str();
-  char* end = nullptr;
-  errno = 0;
-  float v = std::strtof(s, &end);
-  if (end == s) return false;
-  *out = v;
-  return true;
-}
-
 struct Face {
   uint32_t v[3];
   uint32_t t[3] = {0, 0, 0};  // vt indices, valid when t_ok (IsTextureIdxsValid)
@@ -89,10 +76,10 @@ bool ParseOBJ(const std::string& path, std::vector<Vec3>* vertices, std::vector<
     ls >> prefix;
     if (prefix == "v") {
       Vec3 v;
-      if (ReadFloat(ls, &v.x) && ReadFloat(ls, &v.y) && ReadFloat(ls, &v.z)) vertices->push_back(v);
+      if (ls >> v.x >> v.y >> v.z) vertices->push_back(v);  // libstdc++ num_get, as the reference
     } else if (prefix == "vt") {  // model_loader.cpp:65-71
       float a, b;
-      if (ReadFloat(ls, &a) && ReadFloat(ls, &b)) uvs->emplace_back(a, b);
+      if (ls >> a >> b) uvs->emplace_back(a, b);
     } else if (prefix == "f") {  // model_loader.cpp:82-143: v/vt/vn per corner
       std::vector<uint32_t> vi, ti;
       std::string tok;
@@ -187,15 +174,15 @@ void ParseMTL(const std::string& folder, const std::string& file_name, std::vect
       m.texture_path = folder + "/" + tex;
     } else if (prefix == "Kd") {
       Vec3 d;
-      ReadFloat(ls, &d.x) && ReadFloat(ls, &d.y) && ReadFloat(ls, &d.z);
+      ls >> d.x >> d.y >> d.z;  // the reference's glm::vec3 is indeterminate where nothing is read: 0 here
       m.diffuse = d;
     } else if (prefix == "Ks") {
       Vec3 s;
-      ReadFloat(ls, &s.x) && ReadFloat(ls, &s.y) && ReadFloat(ls, &s.z);
+      ls >> s.x >> s.y >> s.z;
       m.specular = s;
     } else if (prefix == "Ns") {
       float e = 0.f;
-      ReadFloat(ls, &e);
+      ls >> e;
       m.specular_ex = e;
     }
   }
