@@ -8,13 +8,14 @@ dispatches on the CPU (see srt_oracle.h).
 from __future__ import annotations
 
 import ctypes as C
+import os
 import pathlib
 import subprocess
 
 import numpy as np
 
 ORACLE_DIR = pathlib.Path(__file__).resolve().parent
-LIB = ORACLE_DIR / "_build" / "liboracle.so"
+LIB = pathlib.Path(os.environ.get("ORACLE_LIB_PATH", ORACLE_DIR / "_build" / "liboracle.so"))
 
 P = C.c_void_p
 
