@@ -120,7 +120,12 @@ int srt_get_stats(srt_context* ctx, srt_stats* out);
 /* Device time of the path-tracing kernel launches of the last render call
  * (HIP events on the context's stream around each sample_kernel launch). */
 int srt_last_kernel_ms(srt_context* ctx, float* ms);
-int srt_reset_stats(srt_context* ctx);
+int srt_reset_stats(srt_context* ctx);  /* also zeroes the NaN counter */
+/* Failure detection: path samples with a NaN component accumulated since the
+ * context was created or srt_reset_stats (always counted, by the ordered
+ * per-pixel sum).  The reference tests each sample for NaN after adding it to
+ * the accumulation and discards the result (raytrace_compute.glsl:408-410). */
+int srt_nan_samples(srt_context* ctx, uint64_t* out);
 
 /* Row-band sharding for multi-GPU: this context owns bands b of `band_rows`
  * rows with b % nranks == rank; its images hold only those rows, packed in
@@ -166,6 +171,17 @@ int srt_alloc_images(srt_context* ctx);
 int srt_read_accum(srt_context* ctx, float* host_rgba32f, size_t bytes);
 int srt_read_output(srt_context* ctx, uint8_t* host_rgba8, size_t bytes);
 int srt_write_accum(srt_context* ctx, const float* host_rgba32f, size_t bytes);
+/* Checkpoint / resume of a progressive render (the reference has none: its
+ * accumulation lives in a GL texture).  save writes the accumulation image
+ * (this context's local rows), accumFrames and the camera uniforms, with
+ * CRC32s, to `path` (via a temporary file, so an old checkpoint survives a
+ * failed save).  load checks that the frame size and tiling match the context
+ * (SRT_ERR_INVALID if not; SRT_ERR_IO for a missing, truncated or corrupt
+ * file), restores the image and the uniforms and returns accumFrames; the
+ * next frames (accumFrames + 1, ...) then continue bit-identically to an
+ * uninterrupted render. */
+int srt_checkpoint_save(srt_context* ctx, const char* path);
+int srt_checkpoint_load(srt_context* ctx, const char* path, int32_t* accum_frames);
 /* Output stage (replaces the GL display quad, src/main.cpp:303-349): write an
  * RGBA8 image to `path`, PNG (RGBA) or binary PPM (RGB) by extension.
  * flip_y != 0 writes the kernel's bottom row (j = 0) last, as displayed.

@@ -24,6 +24,7 @@ struct KParams {
   float4* accum;
   uint32_t* out;
   unsigned long long* stats;
+  unsigned long long* nan_ctr;  // path samples with a NaN component (accumulate_kernel; srt_nan_samples)
   uint32_t* batch_ctr;     // next unclaimed 64-item batch of the launch (zeroed before it)
   int tail_start;          // batches from which a claim takes one batch (LaunchSamples)
   int W, H, WH;

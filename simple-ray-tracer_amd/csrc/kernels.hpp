@@ -557,11 +557,16 @@ __global__ __launch_bounds__(256) void accumulate_kernel(KParams kp, int out_fra
   const float4 a0 = kp.accum[li];
   f3 acc = mk(a0.x, a0.y, a0.z);
   const float4* L = kp.lbuf + li;
+  uint32_t nan = 0;
   for (int k = 0; k < kp.nframes; ++k) {
     const float4 s = L[(size_t)k * (size_t)kp.local_pixels];
     acc = acc + mk(s.x, s.y, s.z);
+    nan += ((s.x != s.x) | (s.y != s.y) | (s.z != s.z)) ? 1u : 0u;
   }
   kp.accum[li] = make_float4(acc.x, acc.y, acc.z, 1.0f);
+  // failure detection: the reference tests a sample for NaN after accumulating it and
+  // then discards the result (raytrace_compute.glsl:408-410); here it is counted
+  if (nan) atomicAdd(kp.nan_ctr, (unsigned long long)nan);
   if (kp.write_output) {
     const f3 o = acc / (float)out_frames;
     const uint32_t r = to_unorm8(linearToSrgb(o.x)), g = to_unorm8(linearToSrgb(o.y)),

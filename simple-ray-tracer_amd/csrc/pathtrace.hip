@@ -27,10 +27,13 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 #include <mutex>
 #include <string>
 #include <vector>
+
+#include <zlib.h>
 
 #include "kernels.hpp"
 
@@ -126,6 +129,7 @@ struct srt_context {
   int num_cus = 256;
   // stats
   unsigned long long* d_stats = nullptr;
+  unsigned long long* d_nan = nullptr;  // NaN path samples since the last srt_reset_stats
   srt_stats stats{};
   // per-chunk HIP events around the sample kernel of the last render call
   std::vector<hipEvent_t> ev;
@@ -279,6 +283,7 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
   kp->accum = c->d_accum;
   kp->out = c->d_out;
   kp->stats = c->d_stats;
+  kp->nan_ctr = c->d_nan;
   kp->W = c->W;
   kp->H = c->H;
   kp->WH = c->W * c->H;
@@ -586,7 +591,11 @@ int srt_create(int device, void* stream, srt_context** out) {
     }
     c->own_stream = true;
   }
-  if (hipMalloc(&c->d_stats, sizeof(unsigned long long) * srt::ST_TOTAL) != hipSuccess) {
+  if (hipMalloc(&c->d_stats, sizeof(unsigned long long) * srt::ST_TOTAL) != hipSuccess ||
+      hipMalloc(&c->d_nan, sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(c->d_nan, 0, sizeof(unsigned long long)) != hipSuccess) {
+    FreeDev(c->d_stats);
+    FreeDev(c->d_nan);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
     srt::SetError("hipMalloc(stats) failed");
@@ -602,7 +611,7 @@ int srt_destroy(srt_context* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   FreeDev(c->d_nodes); FreeDev(c->d_tris); FreeDev(c->d_mats); FreeDev(c->d_bvhs); FreeDev(c->d_lights);
   FreeDev(c->d_tex); FreeDev(c->d_tex_info); FreeDev(c->d_tri_uv);
-  FreeDev(c->d_noise_xy); FreeDev(c->d_noise_u); FreeDev(c->d_stats); FreeDev(c->d_lbuf); FreeDev(c->d_gstack);
+  FreeDev(c->d_noise_xy); FreeDev(c->d_noise_u); FreeDev(c->d_stats); FreeDev(c->d_nan); FreeDev(c->d_lbuf); FreeDev(c->d_gstack);
   FreeDev(c->d_batch_ctr); FreeDev(c->d_tile_cost); FreeDev(c->d_tile_order);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (!c->images_external) { FreeDev(c->d_accum); FreeDev(c->d_out); }
@@ -760,6 +769,19 @@ int srt_get_stats(srt_context* c, srt_stats* out) {
 int srt_reset_stats(srt_context* c) {
   if (!c) return SRT_ERR_INVALID;
   c->stats = srt_stats{};
+  HIP_OK(hipSetDevice(c->device));
+  HIP_OK(hipMemsetAsync(c->d_nan, 0, sizeof(unsigned long long), c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  return SRT_OK;
+}
+
+int srt_nan_samples(srt_context* c, uint64_t* out) {
+  if (!c || !out) return SRT_ERR_INVALID;
+  unsigned long long v = 0;
+  HIP_OK(hipSetDevice(c->device));
+  HIP_OK(hipMemcpyAsync(&v, c->d_nan, sizeof(v), hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  *out = v;
   return SRT_OK;
 }
 
@@ -989,6 +1011,90 @@ int srt_write_accum(srt_context* c, const float* host, size_t bytes) {
   if (bytes < need) return SRT_ERR_INVALID;
   HIP_OK(hipMemcpyAsync(c->d_accum, host, need, hipMemcpyHostToDevice, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
+  return SRT_OK;
+}
+
+namespace {
+constexpr char kCkptMagic[8] = {'S', 'R', 'T', 'C', 'K', 'P', 'T', '1'};
+struct CkptHeader {
+  char magic[8];
+  int32_t version, width, local_rows, rank, nranks, band_rows, accum_frames, pad;
+  float cam[12];  // cameraOrigin, cameraDirection, cameraUp, cameraRight
+  uint64_t payload_bytes;
+  uint32_t payload_crc, header_crc;
+};
+uint32_t Crc32(const void* p, size_t n) {
+  return (uint32_t)crc32(0L, static_cast<const Bytef*>(p), (uInt)n);
+}
+}  // namespace
+
+int srt_checkpoint_save(srt_context* c, const char* path) {
+  if (!c || !path || !c->d_accum || c->img_w <= 0 || c->img_rows <= 0) return SRT_ERR_INVALID;
+  std::vector<float> acc((size_t)c->img_w * c->img_rows * 4);
+  int rc = srt_read_accum(c, acc.data(), acc.size() * sizeof(float));
+  if (rc) return rc;
+  CkptHeader h{};
+  std::memcpy(h.magic, kCkptMagic, 8);
+  h.version = 1;
+  h.width = c->img_w;
+  h.local_rows = c->img_rows;
+  h.rank = c->rank;
+  h.nranks = c->nranks;
+  h.band_rows = c->band_rows;
+  h.accum_frames = c->accum_frames;
+  const float* cam[4] = {c->cam_origin, c->cam_dir, c->cam_up, c->cam_right};
+  for (int i = 0; i < 4; ++i) std::memcpy(h.cam + 3 * i, cam[i], 3 * sizeof(float));
+  h.payload_bytes = acc.size() * sizeof(float);
+  h.payload_crc = Crc32(acc.data(), h.payload_bytes);
+  h.header_crc = Crc32(&h, offsetof(CkptHeader, header_crc));
+  const std::string tmp = std::string(path) + ".tmp";
+  FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) {
+    srt::SetError(std::string("srt_checkpoint_save: cannot open ") + tmp);
+    return SRT_ERR_IO;
+  }
+  const bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 && std::fwrite(acc.data(), 1, h.payload_bytes, f) == h.payload_bytes;
+  if (std::fclose(f) != 0 || !ok || std::rename(tmp.c_str(), path) != 0) {  // the old file survives a failed save
+    std::remove(tmp.c_str());
+    srt::SetError(std::string("srt_checkpoint_save: cannot write ") + path);
+    return SRT_ERR_IO;
+  }
+  return SRT_OK;
+}
+
+int srt_checkpoint_load(srt_context* c, const char* path, int32_t* accum_frames) {
+  if (!c || !path || !c->d_accum) return SRT_ERR_INVALID;
+  FILE* f = std::fopen(path, "rb");
+  if (!f) {
+    srt::SetError(std::string("srt_checkpoint_load: cannot open ") + path);
+    return SRT_ERR_IO;
+  }
+  CkptHeader h{};
+  std::vector<float> acc;
+  bool ok = std::fread(&h, sizeof h, 1, f) == 1 && std::memcmp(h.magic, kCkptMagic, 8) == 0 && h.version == 1 &&
+            h.header_crc == Crc32(&h, offsetof(CkptHeader, header_crc));
+  if (ok && (h.width != c->img_w || h.local_rows != c->img_rows || h.rank != c->rank || h.nranks != c->nranks ||
+             h.band_rows != c->band_rows || h.payload_bytes != (uint64_t)c->img_w * c->img_rows * 16)) {
+    std::fclose(f);
+    srt::SetError("srt_checkpoint_load: the checkpoint's frame or tiling differs from the context's");
+    return SRT_ERR_INVALID;
+  }
+  if (ok) {
+    acc.resize(h.payload_bytes / sizeof(float));
+    ok = std::fread(acc.data(), 1, h.payload_bytes, f) == h.payload_bytes &&
+         Crc32(acc.data(), h.payload_bytes) == h.payload_crc;
+  }
+  std::fclose(f);
+  if (!ok) {
+    srt::SetError(std::string("srt_checkpoint_load: not a valid checkpoint (truncated or corrupt): ") + path);
+    return SRT_ERR_IO;
+  }
+  const int rc = srt_write_accum(c, acc.data(), h.payload_bytes);
+  if (rc) return rc;
+  c->accum_frames = h.accum_frames;
+  float* cam[4] = {c->cam_origin, c->cam_dir, c->cam_up, c->cam_right};
+  for (int i = 0; i < 4; ++i) std::memcpy(cam[i], h.cam + 3 * i, 3 * sizeof(float));
+  if (accum_frames) *accum_frames = h.accum_frames;
   return SRT_OK;
 }
 

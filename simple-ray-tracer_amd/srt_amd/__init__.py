@@ -515,6 +515,21 @@ class Compute:
     def reset_stats(self):
         check(lib().srt_reset_stats(self.ctx), "reset_stats")
 
+    def nan_samples(self) -> int:
+        """Path samples with a NaN component since creation / reset_stats (failure detection)."""
+        v = C.c_uint64(0)
+        check(lib().srt_nan_samples(self.ctx, C.byref(v)), "nan_samples")
+        return int(v.value)
+
+    def checkpoint_save(self, path):
+        check(lib().srt_checkpoint_save(self.ctx, str(path).encode()), "checkpoint_save")
+
+    def checkpoint_load(self, path) -> int:
+        """Restores the accumulation image, accumFrames and the camera uniforms; returns accumFrames."""
+        af = C.c_int32(0)
+        check(lib().srt_checkpoint_load(self.ctx, str(path).encode(), C.byref(af)), "checkpoint_load")
+        return int(af.value)
+
     def read_accum(self) -> np.ndarray:
         rows = self.local_rows()
         a = np.zeros((rows, self.width, 4), np.float32)

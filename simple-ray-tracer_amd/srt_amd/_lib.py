@@ -102,6 +102,9 @@ _SIGS = {
     "srt_get_stats": (C.c_int, [P, C.POINTER(Stats)]),
     "srt_last_kernel_ms": (C.c_int, [P, C.POINTER(C.c_float)]),
     "srt_reset_stats": (C.c_int, [P]),
+    "srt_nan_samples": (C.c_int, [P, C.POINTER(C.c_uint64)]),
+    "srt_checkpoint_save": (C.c_int, [P, C.c_char_p]),
+    "srt_checkpoint_load": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_int32)]),
     "srt_set_tiling": (C.c_int, [P, C.c_int, C.c_int, C.c_int]),
     "srt_local_rows": (C.c_int, [P]),
     "srt_upload_scene": (C.c_int, [P, P, C.c_uint32, P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P,
