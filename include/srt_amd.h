@@ -114,7 +114,8 @@ int srt_finish(srt_context* ctx);
  * with accumFrames = frame_first .. frame_first+nframes-1 and
  * resetAccumBuffer = false (bit-identical accum buffer); the RGBA8 image is
  * written once, for the last frame, when write_output != 0.  Counting
- * launches (count != 0) also fill srt_get_stats. */
+ * launches (count != 0) also fill srt_get_stats.  Leaves the accumFrames
+ * uniform at frame_first + nframes - 1, as the last dispatch would. */
 int srt_render_frames(srt_context* ctx, int frame_first, int nframes, int write_output, int count);
 int srt_get_stats(srt_context* ctx, srt_stats* out);
 /* Device time of the path-tracing kernel launches of the last render call

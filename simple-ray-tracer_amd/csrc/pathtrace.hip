@@ -713,7 +713,9 @@ int srt_render_frames(srt_context* c, int frame_first, int nframes, int write_ou
   kp.nframes = nframes;
   kp.write_output = write_output ? 1 : 0;
   kp.reset = 0;
-  return Launch(c, kp, count != 0);
+  rc = Launch(c, kp, count != 0);
+  if (rc == SRT_OK) c->accum_frames = frame_first + nframes - 1;  // the uniform as the last dispatch leaves it
+  return rc;
 }
 
 int srt_finish(srt_context* c) {
