@@ -125,7 +125,7 @@ __device__ __forceinline__ void slot_read(const uint32_t* base, int stride, int 
 // 1.0f / a, correctly rounded, for every a that is not denormal.  v_rcp_f32
 // plus one FMA Newton step equals the correctly rounded quotient for every
 // 2^-126 <= |a| < 2^126 (all 2^32 inputs checked on gfx950:
-// tools/rcp_exhaustive.hip, tests/test_gpu_rcp.py); |a| >= 2^126, inf and NaN
+// tools/rcp_exhaustive.hip, tests/test_gpu_exhaustive_math.py); |a| >= 2^126, inf and NaN
 // take the full division on a branch that is skipped unless some lane of the
 // wave needs it.  Callers must not use the result for denormal a (the
 // triangle test rejects |a| < 1e-4 before f matters).
