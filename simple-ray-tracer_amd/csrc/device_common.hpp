@@ -39,6 +39,10 @@ struct KParams {
   int ext_w, ext_h;
   int stack_entries;
   int nodes_f4, tris_f4;   // LDS-resident scene: sizes of the node / triangle arrays in float4
+  // internal nodes' child index: pairs start at odd slots and an even index (the
+  // pair's start - 1) flags a right child whose own pair follows (pathtrace.hip
+  // LayoutNodes); ref_or = 1 decodes it, 0 for the identity layout (no flags)
+  uint32_t ref_or;
   float4* lbuf;            // sample buffer: nframes x local_pixels radiance samples
   int local_pixels;        // W * local_rows
   int trav_frac16;         // resume shading when fewer than trav_frac16/16 of working lanes traverse

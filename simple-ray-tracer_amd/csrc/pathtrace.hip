@@ -85,6 +85,7 @@ struct srt_context {
   std::vector<srt_bvh_record> h_bvhs;
   std::vector<std::pair<uint32_t, uint32_t>> bvh_tris;  // triangle range [lo, hi) of each record's tree
   uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
+  uint32_t ref_or = 0;  // KParams::ref_or of the uploaded node layout
   // textures (srt_upload_textures) and, when materials sample them, the
   // per-triangle vertex uvs (2 float4: uv0 uv1 | uv2 0 0)
   float4* d_tex = nullptr;
@@ -304,6 +305,7 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
   kp->ext_h = c->H;
   kp->stack_entries = c->stack_entries;
   kp->nodes_f4 = (int)(2 * ((size_t)c->n_nodes + 1));
+  kp->ref_or = c->ref_or;
   kp->tris_f4 = (int)(3 * ((size_t)c->n_tris + srt::kTriPad));  // with the padding records
   CameraParams(c, kp);
   return SRT_OK;
@@ -554,6 +556,60 @@ int ValidateNodes(const srt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_tris, 
   return SRT_OK;
 }
 
+// Device node layout.  An internal step reads the current node's child pair
+// and, speculatively, the pair after it (traversal.hpp, trav_internal): when
+// the right child -- the one the traversal visits first -- is internal and its
+// own child pair is that next pair, the step expands it too, so a descent along
+// right children takes one memory round trip per two levels.  The device array
+// therefore holds the pairs in the traversal's order (pre-order, right child
+// first), where a right child's pair directly follows its parent's.  Only
+// addresses change: every record keeps its bounds, leaf triangle range and
+// count; an internal node's child index and each BVH's root are remapped.  Slot
+// 0 keeps node 0 (the ghost zero records traverse from it); other roots take a
+// pair's first slot with a zero record beside it.  Returns false (the identity
+// layout is used) for inputs whose sibling pairs overlap, which no
+// reference-built tree has; the kernel checks adjacency itself, so any layout
+// stays exact.
+bool LayoutNodes(const srt_bvh_node* nodes, uint32_t n_nodes, const srt_bvh_record* bvhs, uint32_t n_bvhs,
+                 std::vector<uint32_t>* remap, uint32_t* n_slots) {
+  constexpr uint32_t kUnset = 0xFFFFFFFFu;
+  remap->assign(n_nodes, kUnset);
+  auto& m = *remap;
+  m[0] = 0;
+  uint32_t next = 1;  // pairs start at odd slots (64-B aligned behind the 32-B pad)
+  std::vector<uint32_t> roots{0};
+  for (uint32_t b = 0; b < n_bvhs; ++b) {
+    const uint32_t r = bvhs[b].first_index;
+    if (m[r] == kUnset) {
+      m[r] = next;
+      next += 2;
+    }
+    roots.push_back(r);
+  }
+  std::vector<uint32_t> st;
+  for (uint32_t r : roots) {
+    st.push_back(r);
+    while (!st.empty()) {
+      const uint32_t i = st.back();
+      st.pop_back();
+      const srt_bvh_node& n = nodes[i];
+      if (n.prim_count > 0) continue;
+      const uint32_t c0 = n.first_child_or_prim_index, c1 = c0 + 1;
+      if (m[c0] == kUnset && m[c1] == kUnset) {
+        m[c0] = next;
+        m[c1] = next + 1;
+        next += 2;
+        st.push_back(c0);  // popped after c1's subtree: c1 is visited first
+        st.push_back(c1);
+      } else if (m[c0] == kUnset || m[c1] != m[c0] + 1) {
+        return false;  // a shared or overlapping pair
+      }
+    }
+  }
+  *n_slots = next;
+  return true;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -802,16 +858,32 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   int rc = ValidateNodes(nodes, n_nodes, n_tris, bvhs, n_bvhs, &depth, &tri_ranges);
   if (rc) return rc;
   HIP_OK(hipSetDevice(c->device));
-  // nodes: 32-B records behind a 32-B pad so sibling pairs are 64-B aligned
-  std::vector<float4> hn(2 * ((size_t)n_nodes + 1));
-  hn[0] = hn[1] = make_float4(0, 0, 0, 0);
+  // nodes: 32-B records behind a 32-B pad so sibling pairs are 64-B aligned,
+  // in the traversal's order (LayoutNodes; unreachable nodes are dropped), and
+  // one zero pair past the end for the internal step's speculative read
+  std::vector<uint32_t> remap;
+  uint32_t n_slots = n_nodes;
+  const char* lay_env = std::getenv("SRT_NODE_LAYOUT");
+  bool laid = !(lay_env && lay_env[0] == '0') && LayoutNodes(nodes, n_nodes, bvhs, n_bvhs, &remap, &n_slots);
+  if (!laid) {
+    remap.resize(n_nodes);
+    for (uint32_t i = 0; i < n_nodes; ++i) remap[i] = i;
+    n_slots = n_nodes;
+  }
+  std::vector<float4> hn(2 * ((size_t)n_slots + 1 + srt::kNodePad), make_float4(0, 0, 0, 0));
   for (uint32_t i = 0; i < n_nodes; ++i) {
+    if (remap[i] == 0xFFFFFFFFu) continue;
     const srt_bvh_node& n = nodes[i];
+    uint32_t first = n.first_child_or_prim_index;
+    if (n.prim_count == 0) {  // internal: c0's slot, less 1 when c1 is internal (its pair then follows)
+      first = remap[first];
+      if (laid && nodes[n.first_child_or_prim_index + 1].prim_count == 0) first -= 1;
+    }
     float w0, w1;
-    std::memcpy(&w0, &n.first_child_or_prim_index, 4);
+    std::memcpy(&w0, &first, 4);
     std::memcpy(&w1, &n.prim_count, 4);
-    hn[2 * (size_t)i + 2] = make_float4(n.min_bounds[0], n.min_bounds[1], n.min_bounds[2], w0);
-    hn[2 * (size_t)i + 3] = make_float4(n.max_bounds[0], n.max_bounds[1], n.max_bounds[2], w1);
+    hn[2 * (size_t)remap[i] + 2] = make_float4(n.min_bounds[0], n.min_bounds[1], n.min_bounds[2], w0);
+    hn[2 * (size_t)remap[i] + 3] = make_float4(n.max_bounds[0], n.max_bounds[1], n.max_bounds[2], w1);
   }
   // materials -> shading materials (raytrace_utils.glsl:140-175); one zero
   // record appended for out-of-range material indices (OOB SSBO reads = 0)
@@ -881,16 +953,18 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   HIP_OK(hipMemcpyAsync(c->d_tris, ht.data(), ht.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
   c->h_bvhs.assign(bvhs, bvhs + n_bvhs);
+  for (auto& r : c->h_bvhs) r.first_index = remap[r.first_index];  // roots in the device layout
   c->bvh_tris = std::move(tri_ranges);
   c->sample_textures = sampled;
   c->bvhs_dirty = true;
-  c->n_nodes = n_nodes;
+  c->n_nodes = n_slots + srt::kNodePad;
+  c->ref_or = laid ? 1u : 0u;
   c->n_tris = n_tris;
   c->n_mats = n_mats;
   c->stack_entries = depth + 1;
   uint32_t max_leaf = 0;
   for (uint32_t i = 0; i < n_nodes; ++i) max_leaf = std::max(max_leaf, nodes[i].prim_count);
-  c->lds_ok = n_tris < (1u << 24) && n_nodes < (1u << 24) && max_leaf < 256;
+  c->lds_ok = n_tris < (1u << 24) && n_slots + srt::kNodePad < (1u << 24) && max_leaf < 256;
   c->scene_ok = true;
   if (c->bvh_count == 0) c->bvh_count = n_bvhs;
   // the zero records beyond n_bvhs traverse from node 0 with a zero ray
@@ -1158,6 +1232,7 @@ int srt_trace_closest(srt_context* c, const srt_ray* rays, uint32_t n, uint32_t*
   int rc = EnsureBvhs(c);
   if (rc) return rc;
   kp.nodes = c->d_nodes;
+  kp.ref_or = c->ref_or;
   kp.tris = c->d_tris;
   kp.bvhs = c->d_bvhs;
   kp.bvh_count = c->bvh_count;

@@ -221,7 +221,7 @@ __device__ uint32_t traverse(const KParams& kp, const Lane& ln, Counters& c, uin
       // internal: test both children now.  The reference pushes c0 then c1
       // and pops c1 first; a child whose box fails is never needed (the
       // distance only shrinks), a lone passing child is visited directly.
-      const uint32_t pi = 2 * ref + 2;
+      const uint32_t pi = 2 * (ref | kp.ref_or) + 2;
       const float4 l0 = node4<LDSM>(kp, pi), h0 = node4<LDSM>(kp, pi + 1);
       const float4 l1 = node4<LDSM>(kp, pi + 2), h1 = node4<LDSM>(kp, pi + 3);
       bump<COUNT>(c, ST_NODES, 2);
@@ -319,6 +319,17 @@ constexpr int kShortStack = SRT_SHORT_STACK;
 constexpr int kClaim = SRT_CLAIM;
 static_assert((kShortStack & (kShortStack - 1)) == 0, "kShortStack must be a power of two");
 constexpr int kTriPad = 3;                // zero records past the triangle array (>= kLeafTris - 1)
+constexpr uint32_t kNodePad = 2;          // zero node records past the array: the speculative next-pair read
+// Internal steps expand the right child in the same step when its child pair
+// is the next pair of the array (trav_internal; pathtrace.hip LayoutNodes).
+#ifndef SRT_SPINE
+#define SRT_SPINE 1
+#endif
+// Global-scene mode only: it waits on memory; the LDS-resident kernel is bound by
+// VALU issue, and the second level's box tests cost it more than the LDS latency
+// they hide (5,676 -> 5,239 Mrays/s on Rubik 1080p).
+template <bool LDSM>
+constexpr bool kSpine = SRT_SPINE && !LDSM;
 static_assert(kLeafTris >= 1 && kLeafTris - 1 <= kTriPad, "kLeafTris");
 
 // Sets up BVH `t.bi` for the world ray (the reference's per-model transform,
@@ -384,9 +395,18 @@ __device__ __forceinline__ void trav_leaf(const KParams& kp, Counters& c, Trav& 
 // c1 if it passes, else to c0 if it passes.
 template <bool COUNT, bool LDSM, bool PACK>
 __device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln, Counters& c, Trav& t) {
-  const uint32_t pi = 2 * t.ref + 2;
+  const uint32_t ref0 = t.ref | kp.ref_or;  // the child pair's first slot
+  const bool spine = kSpine<LDSM> && (ref0 != t.ref);  // c1 is internal and its pair follows
+  const uint32_t pi = 2 * ref0 + 2;
   const float4 l0 = node4<LDSM>(kp, pi), h0 = node4<LDSM>(kp, pi + 1);
   const float4 l1 = node4<LDSM>(kp, pi + 2), h1 = node4<LDSM>(kp, pi + 3);
+  float4 m0, g0, m1, g1;  // c1's child pair
+  if (spine) {
+    m0 = node4<LDSM>(kp, pi + 4);
+    g0 = node4<LDSM>(kp, pi + 5);
+    m1 = node4<LDSM>(kp, pi + 6);
+    g1 = node4<LDSM>(kp, pi + 7);
+  }
   bump<COUNT>(c, ST_NODES, 2);
   float b0, b1;
   const bool v0 = box_test(t.o, t.inv, l0, h0, t.dist, b0);
@@ -394,24 +414,47 @@ __device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln,
   const uint32_t r0 = __float_as_uint(l0.w), n0 = __float_as_uint(h0.w);
   // the c0 slot is written unconditionally (it is free either way; the stack
   // holds depth + 1 entries, validated at upload)
-  if constexpr (LDSM) {
-    slot_write<true>(ln.stk, ln.stride, t.sp, r0, n0, b0);
-  } else {
-    if (t.sp - t.lo == kShortStack) {  // ring full: its oldest entry moves to HBM (rare)
-      uint32_t r, n;
-      float bt;
-      slot_read<PACK>(ln.stk, ln.stride, t.lo & (kShortStack - 1), r, n, bt);
-      slot_write<PACK>(ln.gstk, ln.gstride, t.lo, r, n, bt);
-      ++t.lo;
+  auto push_entry = [&](uint32_t r_, uint32_t n_, float b_) {
+    if constexpr (LDSM) {
+      slot_write<true>(ln.stk, ln.stride, t.sp, r_, n_, b_);
+    } else {
+      if (t.sp - t.lo == kShortStack) {  // ring full: its oldest entry moves to HBM (rare)
+        uint32_t r, n;
+        float bt;
+        slot_read<PACK>(ln.stk, ln.stride, t.lo & (kShortStack - 1), r, n, bt);
+        slot_write<PACK>(ln.gstk, ln.gstride, t.lo, r, n, bt);
+        ++t.lo;
+      }
+      slot_write<PACK>(ln.stk, ln.stride, t.sp & (kShortStack - 1), r_, n_, b_);
     }
-    slot_write<PACK>(ln.stk, ln.stride, t.sp & (kShortStack - 1), r0, n0, b0);
-  }
+  };
+  push_entry(r0, n0, b0);
   t.sp += (v0 & v1) ? 1 : 0;
   if constexpr (COUNT) {
     if ((uint32_t)t.sp > c.v[ST_MAXSTACK]) c.v[ST_MAXSTACK] = (uint32_t)t.sp;
   }
   t.ref = v1 ? __float_as_uint(l1.w) : r0;
   t.cnt = v1 ? __float_as_uint(h1.w) : (v0 ? n0 : kNoneCnt);
+  if constexpr (kSpine<LDSM>) {
+    // The reference pops c1 right after pushing it and re-tests its box with
+    // the unchanged distance (it passes), so when c1 is internal its expansion
+    // is the lane's next step.  Its child pair was read with this node's (the
+    // layout puts it next): expand it now -- one memory round trip for two levels.
+    if (v1 & spine) {
+      bump<COUNT>(c, ST_NODES, 2);
+      float e0, e1;
+      const bool w0 = box_test(t.o, t.inv, m0, g0, t.dist, e0);
+      const bool w1 = box_test(t.o, t.inv, m1, g1, t.dist, e1);
+      const uint32_t s0 = __float_as_uint(m0.w), k0 = __float_as_uint(g0.w);
+      push_entry(s0, k0, e0);
+      t.sp += (w0 & w1) ? 1 : 0;
+      if constexpr (COUNT) {
+        if ((uint32_t)t.sp > c.v[ST_MAXSTACK]) c.v[ST_MAXSTACK] = (uint32_t)t.sp;
+      }
+      t.ref = w1 ? __float_as_uint(m1.w) : s0;
+      t.cnt = w1 ? __float_as_uint(g1.w) : (w0 ? k0 : kNoneCnt);
+    }
+  }
 }
 
 // Nothing current: pop one entry (visited if it still beats the running
