@@ -571,7 +571,7 @@ int ValidateNodes(const srt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_tris, 
 // reference-built tree has; the kernel checks adjacency itself, so any layout
 // stays exact.
 bool LayoutNodes(const srt_bvh_node* nodes, uint32_t n_nodes, const srt_bvh_record* bvhs, uint32_t n_bvhs,
-                 std::vector<uint32_t>* remap, uint32_t* n_slots) {
+                 bool align, std::vector<uint32_t>* remap, uint32_t* n_slots) {
   constexpr uint32_t kUnset = 0xFFFFFFFFu;
   remap->assign(n_nodes, kUnset);
   auto& m = *remap;
@@ -586,6 +586,10 @@ bool LayoutNodes(const srt_bvh_node* nodes, uint32_t n_nodes, const srt_bvh_reco
     }
     roots.push_back(r);
   }
+  // `align`: a chain of right-child pairs starts on a 128-B line (slot = 3 mod
+  // 4: a zero pair pads before it when needed), so a step that reads a pair and
+  // its right child's pair touches one line (see srt_upload_scene for when).
+  uint32_t chain_next = kUnset;  // the node whose pair continues the current chain
   std::vector<uint32_t> st;
   for (uint32_t r : roots) {
     st.push_back(r);
@@ -596,9 +600,11 @@ bool LayoutNodes(const srt_bvh_node* nodes, uint32_t n_nodes, const srt_bvh_reco
       if (n.prim_count > 0) continue;
       const uint32_t c0 = n.first_child_or_prim_index, c1 = c0 + 1;
       if (m[c0] == kUnset && m[c1] == kUnset) {
+        if (align && i != chain_next && nodes[c1].prim_count == 0 && (next & 3u) != 3u) next += 2;
         m[c0] = next;
         m[c1] = next + 1;
         next += 2;
+        chain_next = nodes[c1].prim_count == 0 ? c1 : kUnset;
         st.push_back(c0);  // popped after c1's subtree: c1 is visited first
         st.push_back(c1);
       } else if (m[c0] == kUnset || m[c1] != m[c0] + 1) {
@@ -864,7 +870,16 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   std::vector<uint32_t> remap;
   uint32_t n_slots = n_nodes;
   const char* lay_env = std::getenv("SRT_NODE_LAYOUT");
-  bool laid = !(lay_env && lay_env[0] == '0') && LayoutNodes(nodes, n_nodes, bvhs, n_bvhs, &remap, &n_slots);
+  // Line-aligned chains pay where the tree streams from HBM: fewer lines per
+  // step (C5, 10 M triangles: 505 -> 578 Mrays/s; 3 M: 774 -> 823).  A scene
+  // the 256-MB Infinity Cache holds runs latency-bound and is faster dense
+  // (300 k: 1929 vs 1695; 1 M: 1234 vs 1088), though it then misses more
+  // often in L2.  Measured crossover between 100 and 300 MB of nodes +
+  // triangles; SRT_NODE_ALIGN=1/0 forces either.
+  const char* al_env = std::getenv("SRT_NODE_ALIGN");
+  const double scene_mb = (32.0 * n_nodes + 48.0 * n_tris) / (1 << 20);
+  const bool align = al_env ? al_env[0] == '1' : scene_mb >= 192.0;
+  bool laid = !(lay_env && lay_env[0] == '0') && LayoutNodes(nodes, n_nodes, bvhs, n_bvhs, align, &remap, &n_slots);
   if (!laid) {
     remap.resize(n_nodes);
     for (uint32_t i = 0; i < n_nodes; ++i) remap[i] = i;

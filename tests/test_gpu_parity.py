@@ -189,6 +189,23 @@ def test_synthetic_mesh_global_mode():
     assert_parity(setup, 2)
 
 
+@pytest.mark.parametrize("env", [{"SRT_NODE_ALIGN": "1"}, {"SRT_NODE_LAYOUT": "0"}])
+def test_node_layouts_global_mode(monkeypatch, env):
+    """The device node layouts (pathtrace.hip LayoutNodes): line-aligned right-child chains (chosen for
+    scenes past the Infinity Cache) and the reference's own order (no right-spine double steps) render
+    the oracle's frame in global-scene mode, two models with a moved second one included."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    setup = R.make_setup(48, 40, show_model=True, models=[R.synthetic_model(30000, seed=3)])
+    assert_parity(setup, 2)
+    two = R.make_setup(40, 32, show_model=True, models=[R.synthetic_model(20000, seed=4),
+                                                        R.synthetic_model(5000, seed=6)])
+    frame = np.eye(4, dtype=np.float32)
+    frame[3, :3] = (1.5, -2.0, 0.5)
+    two.scene.bvhs[1]["frame"] = frame.reshape(16)
+    assert_parity(two, 2)
+
+
 def test_lds_and_global_modes_agree(rubik, monkeypatch):
     setup = R.make_setup(64, 48, show_model=True, models=[rubik])
     a, o, _ = gpu_render(setup, 3)

@@ -1,14 +1,13 @@
 #!/bin/bash
-# PMC passes on the C5 synthetic scene (global-scene mode), reduced frame
+# PMC passes of the C5 workload (synthetic 10M triangles, 4096^2 @16 spp, one timed launch) for
+# profiles/counters.json (tools/pmc_roofline.py <dir> --workload synthetic10000000_4096x4096_16spp).
 cd /root/repo && export TMPDIR=/tmp
-TAG=${TAG:-pmc_c5}; A="--scene synthetic --width 2048 --height 2048 --spp 4 --steps 1 --warmup 0 --no-cpu-baseline"
-run() { local name=$1; shift
-  timeout -k 10 600 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/$TAG/$name -o run -- \
-    python bench.py $A > gpurun_out/$TAG/$name.log 2>&1; }
-mkdir -p gpurun_out/$TAG
-run p1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY && \
-run p2 SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_VMEM_WR && \
-run p3 FETCH_SIZE && run p4 WRITE_SIZE && \
-run p5 TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum && \
-run p6 TA_BUSY_avr TA_TA_BUSY_sum TD_BUSY_sum TCP_PENDING_STALL_CYCLES_sum
-echo "pmc exit $?"
+O=${O:-gpurun_out/c5pmc}; mkdir -p $O
+B="python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-global-leg --scene synthetic --width 4096 --height 4096 --spp 16"
+timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT \
+  SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_sq -o run -- \
+  $B > $O/pmc_sq.log 2>&1 && \
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- $B > $O/pmc_fetch.log 2>&1 && \
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- $B > $O/pmc_write.log 2>&1 && \
+timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $O/pmc_tcc -o run -- $B > $O/pmc_tcc.log 2>&1
+rc=$?; echo "pmc exit $rc"; exit $rc

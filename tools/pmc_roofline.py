@@ -1,6 +1,7 @@
 """Writes profiles/counters.json from a round's rocprofv3 PMC passes (tools/profile_round.sh).
 
-usage: python tools/pmc_roofline.py gpurun_out/r02 [--tag r02]
+usage: python tools/pmc_roofline.py gpurun_out/r02 [--tag r02] [--workload NAME]
+(--workload: a single-leg run, e.g. tools/pmc_c5.sh's, whose global-scene instance is NAME)
 
 Each pass ran `python bench.py --steps 1 --warmup 0 --no-cpu-baseline`, so every leg's timed step
 launched its sample_kernel<false, ...> instance exactly once (the counting run is the <true, ...>
@@ -18,12 +19,17 @@ import sys
 
 out_dir = pathlib.Path(sys.argv[1])
 tag = sys.argv[sys.argv.index("--tag") + 1] if "--tag" in sys.argv else out_dir.name
+only = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else None
 root = pathlib.Path(__file__).resolve().parent.parent
 
 LEGS = {  # kernel instance -> workload name bench.py reports
     "void srt::sample_kernel<false, true, true, 1024, false>": "rubik_1920x1080_256spp",
     "void srt::sample_kernel<false, false, true, 256, false>": "synthetic1000000_1920x1080_16spp",
 }
+
+
+if only:
+    LEGS = {"void srt::sample_kernel<false, false, true, 256, false>": only}
 
 
 def rows(sub):
@@ -55,6 +61,9 @@ for wl in sq:
     d["FETCH_SIZE"] = fetch[wl]["FETCH_SIZE"]
     d["WRITE_SIZE"] = write[wl]["WRITE_SIZE"]
     d["hbm_bytes"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
+    if (out_dir / "pmc_tcc").exists():
+        tcc = per_launch("pmc_tcc").get(wl, {})
+        d.update({k: v for k, v in tcc.items()})
     d["source"] = (f"rocprofv3 --pmc passes ({tag}): SQ counters + GRBM_GUI_ACTIVE, FETCH_SIZE, WRITE_SIZE; "
                    f"python bench.py --steps 1 --warmup 0 --no-cpu-baseline; per launch of the timed step")
     data[wl] = d
