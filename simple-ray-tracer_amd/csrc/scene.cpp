@@ -554,8 +554,10 @@ bool DecodePngTexture(const std::string& path, Texture* out, std::string* err) {
 // (shading.hpp texture_sample) and the oracle: fp32 in source order, a
 // non-finite coordinate reads as 0, REPEAT as s - floor(s), texel centres at
 // (i + 0.5) / size, texels c / 255, and the four weighted texels summed
-// (00 + 10) + 01 + 11.  GL_RED samples as (r, 0, 0); a 2-channel file, which
-// the reference uploads as GL_RGB, as (r, g, 0).
+// (00 + 10) + 01 + 11.  GL_RED samples as (r, 0, 0).  A 2-channel file has no
+// defined result in the reference: it uploads the 2-byte texels as GL_RGB
+// (gpu_texture.h:39-52), so GL reads byte triples past the image; here it
+// samples as (r, g, 0).
 void TextureSample(const uint8_t* texels, int width, int height, int channels, float s, float t, float rgb[3]) {
   if (!(std::fabs(s) <= 3.402823466e38f)) s = 0.0f;
   if (!(std::fabs(t) <= 3.402823466e38f)) t = 0.0f;
