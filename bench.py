@@ -119,7 +119,7 @@ def load_counters(workload: str):
         return None
 
 
-def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str) -> dict:
+def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str, global_mode: bool = False) -> dict:
     """Roofs of the dominant kernel, fractions of the live kernel time (HIP events on the launch stream):
     VALU issue (SQ_INSTS_VALU x 2 cycles per SIMD-32 over 1024 SIMDs), LDS-array cycles
     (SQ_LDS_IDX_ACTIVE over 256 CUs), HBM (corrected FETCH_SIZE + WRITE_SIZE over 8 TB/s).  The counters
@@ -156,8 +156,11 @@ def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str) -> di
         "counters_source": cnt.get("source", ""),
         "note": "frac = the bound roof's fraction at the live kernel time; per-launch counters from the committed "
                 "rocprofv3 passes of this workload (profiles/counters.json). The 2.4 GHz peak clock makes every "
-                "fraction a lower bound. algorithmic_GBps = SURVEY 8d bytes per launch / kernel time: the scene "
-                "is read from LDS/L2, so it is not an HBM rate.",
+                "fraction a lower bound. " + (
+                    "hbm = the L2 misses' bytes (2 x FETCH_SIZE + WRITE_SIZE), served by the Infinity Cache or HBM; "
+                    "algorithmic_GBps = SURVEY 8d bytes per launch / kernel time (L2 hits included)." if global_mode
+                    else "algorithmic_GBps = SURVEY 8d bytes per launch / kernel time: the scene is read from LDS "
+                         "and the noise from L2, so it is not an HBM rate."),
     })
     return r
 
@@ -323,14 +326,15 @@ def main(argv=None):
                 "unit": "Mrays/s", "ms_per_step": round(g_el * 1e3 / args.steps, 3),
                 "config": {"scene": f"synthetic {args.global_tris} triangles (SURVEY 8d generator)", "width": 1920,
                            "height": 1080, "spp": args.global_spp, "max_depth": 5},
-                "roofline": roofline(gname, g_k, algorithmic_bytes(g_st) if world == 1 else 0, KERNEL_GLOBAL),
+                "roofline": roofline(gname, g_k, algorithmic_bytes(g_st) if world == 1 else 0, KERNEL_GLOBAL,
+                                     global_mode=True),
             })
 
     if rank == 0:
         ms_per_step = elapsed_s * 1e3 / args.steps
         value = total_rays * args.steps / elapsed_s / 1e6
         k_ms = float(np.mean(kernel_ms))
-        kname = KERNEL_LDS if args.scene == "rubik" else "srt::sample_kernel<false, ...>"
+        kname = {"rubik": KERNEL_LDS, "synthetic": KERNEL_GLOBAL}.get(args.scene, "srt::sample_kernel<false, ...>")
         line = {
             "metric": "Mrays/s (CheckHit queries: camera + bounce + shadow rays) at the BASELINE frame/spp",
             "value": round(value, 3),
@@ -356,7 +360,8 @@ def main(argv=None):
             "msamples_per_s": round(W * H * spp * args.steps / elapsed_s / 1e6, 3),
             "rays_per_step": int(total_rays),
             # per-rank counters describe rank 0's launch: the roofline is a 1-GPU figure
-            "roofline": roofline(wl_name, k_ms, algorithmic_bytes(st), kname) if world == 1 else
+            "roofline": roofline(wl_name, k_ms, algorithmic_bytes(st), kname, global_mode=args.scene == "synthetic")
+            if world == 1 else
             {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
              "kernel_ms": round(k_ms, 3), "note": "roofline reported at N=1"},
             "legs": legs,
