@@ -11,10 +11,12 @@ sampled frames (one fused kernel launch) and, for N > 1, the gather of every
 rank's row bands to rank 0 (RCCL over xGMI) plus the root-side assembly of the
 frame.  Inputs (scene, noise buffers, lights) are resident in HBM before timing.
 
-A second leg ("global_scene") times the real-mesh path: a synthetic 1 M-triangle
-mesh (SURVEY.md 8d generator) too large for the LDS scene copy, traversed from
-HBM/L2, at 1920x1080 and 16 spp.  It is reported under "legs" with its own
-roofline; `value` is the main leg.
+Two more legs time the real-mesh path (scenes too large for the LDS scene copy,
+traversed from HBM/L2), each under "legs" with its own roofline; `value` is the
+main leg:
+  global_scene  a synthetic 1 M-triangle soup (SURVEY.md 8d generator), 1920x1080 @16 spp;
+  surface_mesh  a closed 262k-triangle surface (torus-knot tube, the stand-in for a
+                mesh such as the absent Airplane OBJ), 1920x1080 @64 spp.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -50,7 +52,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default="rubik", choices=("rubik", "spheres", "synthetic"))
+    ap.add_argument("--scene", default="rubik", choices=("rubik", "spheres", "synthetic", "torusknot"))
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=256)
@@ -62,6 +64,8 @@ def parse(argv=None):
     ap.add_argument("--no-global-leg", action="store_true", help="skip the 1 M-triangle global-scene leg")
     ap.add_argument("--global-tris", type=int, default=1_000_000)
     ap.add_argument("--global-spp", type=int, default=16)
+    ap.add_argument("--no-surface-leg", action="store_true", help="skip the 262k-triangle surface-mesh leg")
+    ap.add_argument("--surface-spp", type=int, default=64)
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (multi-rank tests on one GPU)")
     ap.add_argument("--dump", default=None, help="rank 0 saves the assembled frame (npz) after the last step")
@@ -174,6 +178,9 @@ def build_setup(scene: str, W: int, H: int, spp: int, max_depth: int, synthetic_
     elif scene == "synthetic":
         models = [R.synthetic_model(synthetic_tris)]
         show_model, wl = True, f"synthetic{synthetic_tris}_{W}x{H}_{spp}spp"
+    elif scene == "torusknot":
+        models = [R.torus_knot_model()]
+        show_model, wl = True, f"torusknot262144_{W}x{H}_{spp}spp"
     else:
         models, show_model, wl = None, False, f"spheres_{W}x{H}_{spp}spp"
     if max_depth != 5:
@@ -328,6 +335,22 @@ def main(argv=None):
                            "height": 1080, "spp": args.global_spp, "max_depth": 5},
                 "roofline": roofline(gname, g_k, algorithmic_bytes(g_st) if world == 1 else 0, KERNEL_GLOBAL,
                                      global_mode=True),
+            })
+
+    if not args.no_surface_leg:
+        ssetup, sname = build_setup("torusknot", 1920, 1080, args.surface_spp, 5, 0)
+        s_el, s_rays, s_st, s_kms, s_run = run_leg(ssetup, args.surface_spp, args, rank=rank, world=world,
+                                                   device=device, stream=stream)
+        s_run.close()
+        if rank == 0:
+            legs.append({
+                "leg": "surface_mesh", "workload": sname, "value": round(s_rays * args.steps / s_el / 1e6, 3),
+                "unit": "Mrays/s", "ms_per_step": round(s_el * 1e3 / args.steps, 3),
+                "config": {"scene": "torus-knot tube, 262144 triangles (closed surface mesh; srt_amd.render."
+                                    "torus_knot_triangles), model camera and lights", "width": 1920, "height": 1080,
+                           "spp": args.surface_spp, "max_depth": 5},
+                "roofline": roofline(sname, float(np.mean(s_kms)), algorithmic_bytes(s_st) if world == 1 else 0,
+                                     KERNEL_GLOBAL, global_mode=True),
             })
 
     if rank == 0:

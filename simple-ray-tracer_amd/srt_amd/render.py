@@ -145,5 +145,37 @@ def synthetic_triangles(n_tris: int, seed: int = 0x5EED2025) -> np.ndarray:
     return tri.reshape(n_tris, 9)
 
 
+def torus_knot_triangles(n_u: int = 512, n_v: int = 256, p: int = 2, q: int = 3) -> np.ndarray:
+    """A closed surface mesh for the global-scene path (the Airplane OBJ is absent): a (p, q) torus-knot tube,
+    2 * n_u * n_v triangles, centred at (0, 9, 0) in the Rubik's extent (~18 units across) so the model camera
+    and lights of src/main.cpp frame it.  Deterministic (float64 numpy, rounded once to float32)."""
+    u = np.arange(n_u, dtype=np.float64) * (2.0 * np.pi / n_u)
+    v = np.arange(n_v, dtype=np.float64) * (2.0 * np.pi / n_v)
+
+    def curve(t):
+        r = 6.0 + 2.6 * np.cos(q * t)
+        return np.stack([r * np.cos(p * t), 9.0 + r * np.sin(p * t), 4.0 * np.sin(q * t)], axis=-1)
+
+    c = curve(u)
+    tang = curve(u + 1e-4) - curve(u - 1e-4)
+    tang /= np.linalg.norm(tang, axis=-1, keepdims=True)
+    up = np.array([0.0, 0.0, 1.0])
+    n1 = np.cross(tang, up)
+    n1 /= np.linalg.norm(n1, axis=-1, keepdims=True)
+    n2 = np.cross(tang, n1)
+    rad = 2.4
+    pts = (c[:, None, :] + rad * (np.cos(v)[None, :, None] * n1[:, None, :] + np.sin(v)[None, :, None] * n2[:, None, :]))
+    i0 = np.arange(n_u)[:, None]
+    j0 = np.arange(n_v)[None, :]
+    i1, j1 = (i0 + 1) % n_u, (j0 + 1) % n_v
+    a, b, cc, d = pts[i0, j0], pts[i1, j0], pts[i1, j1], pts[i0, j1]
+    tri = np.stack([np.stack([a, b, cc], axis=-2), np.stack([a, cc, d], axis=-2)], axis=2)  # (n_u, n_v, 2, 3, 3)
+    return tri.reshape(-1, 9).astype(np.float32)
+
+
+def torus_knot_model(n_u: int = 512, n_v: int = 256) -> Model:
+    return model_from_triangles(torus_knot_triangles(n_u, n_v), kd=(0.8, 0.6, 0.3), ks=(0.5, 0.5, 0.5), ns=40.0)
+
+
 def synthetic_model(n_tris: int, seed: int = 0x5EED2025) -> Model:
     return model_from_triangles(synthetic_triangles(n_tris, seed), kd=(0.8, 0.8, 0.8), ks=(0.0, 0.0, 0.0), ns=10.0)

@@ -189,6 +189,12 @@ def test_synthetic_mesh_global_mode():
     assert_parity(setup, 2)
 
 
+def test_surface_mesh_global_mode():
+    """bench.py's surface_mesh leg: the 262k-triangle torus-knot tube (global-scene mode) against the oracle."""
+    setup = R.make_setup(64, 40, show_model=True, models=[R.torus_knot_model()])
+    assert_parity(setup, 2)
+
+
 @pytest.mark.parametrize("env", [{"SRT_NODE_ALIGN": "1"}, {"SRT_NODE_LAYOUT": "0"}])
 def test_node_layouts_global_mode(monkeypatch, env):
     """The device node layouts (pathtrace.hip LayoutNodes): line-aligned right-child chains (chosen for

@@ -22,14 +22,15 @@ tag = sys.argv[sys.argv.index("--tag") + 1] if "--tag" in sys.argv else out_dir.
 only = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else None
 root = pathlib.Path(__file__).resolve().parent.parent
 
-LEGS = {  # kernel instance -> workload name bench.py reports
-    "void srt::sample_kernel<false, true, true, 1024, false>": "rubik_1920x1080_256spp",
-    "void srt::sample_kernel<false, false, true, 256, false>": "synthetic1000000_1920x1080_16spp",
+LEGS = {  # kernel instance -> the workloads bench.py runs on it, in launch order (one timed launch each)
+    "void srt::sample_kernel<false, true, true, 1024, false>": ["rubik_1920x1080_256spp"],
+    "void srt::sample_kernel<false, false, true, 256, false>": ["synthetic1000000_1920x1080_16spp",
+                                                                "torusknot262144_1920x1080_64spp"],
 }
 
 
 if only:
-    LEGS = {"void srt::sample_kernel<false, false, true, 256, false>": only}
+    LEGS = {"void srt::sample_kernel<false, false, true, 256, false>": [only]}
 
 
 def rows(sub):
@@ -38,18 +39,17 @@ def rows(sub):
 
 
 def per_launch(sub):
-    """{workload: {counter: value}} of each leg's last dispatch (summed over the dimensions rocprofv3 splits)."""
+    """{workload: {counter: value}} of each leg's dispatch (summed over the dimensions rocprofv3 splits)."""
     out = {}
-    for leg_kernel, wl in LEGS.items():
+    for leg_kernel, wls in LEGS.items():
         rs = [r for r in rows(sub) if r["Kernel_Name"].startswith(leg_kernel)]
-        if not rs:
-            continue
-        last = max(int(r["Dispatch_Id"]) for r in rs)
-        agg = {}
-        for r in rs:
-            if int(r["Dispatch_Id"]) == last:
-                agg[r["Counter_Name"]] = agg.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-        out[wl] = agg
+        ids = sorted({int(r["Dispatch_Id"]) for r in rs})
+        for wl, did in zip(wls, ids[-len(wls):] if len(ids) >= len(wls) else ids):
+            agg = {}
+            for r in rs:
+                if int(r["Dispatch_Id"]) == did:
+                    agg[r["Counter_Name"]] = agg.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+            out[wl] = agg
     return out
 
 
