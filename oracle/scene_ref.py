@@ -124,6 +124,26 @@ def _round_f32(text: str) -> np.float32:
     return -r if neg else r
 
 
+def fma_f32(a, b, c) -> np.float32:
+    """fmaf(a, b, c) for float32 operands: the exact a*b + c rounded once to nearest-even float32."""
+    q = Fraction(float(np.float32(a))) * Fraction(float(np.float32(b))) + Fraction(float(np.float32(c)))
+    if q == 0:
+        return F(0.0) if (np.float32(a) * np.float32(b) + np.float32(c)) >= 0 else F(-0.0)
+    return _round_frac_f32(q)
+
+
+def _round_frac_f32(q: Fraction) -> np.float32:
+    a = abs(q)
+    if a >= Fraction(2 ** 103) * (2 ** 25 - 1):
+        r = F(np.inf)
+    else:
+        c = np.float32(float(a))
+        with np.errstate(over="ignore"):
+            cands = [x for x in (c, np.nextafter(c, F(0)), np.nextafter(c, F(np.inf))) if np.isfinite(x)]
+        r = min(cands, key=lambda x: (abs(Fraction(float(x)) - a), int(np.array(x).view(np.uint32)) & 1))
+    return -r if q < 0 else r
+
+
 def istream_floats(rest: str, n: int):
     """`ls >> f1 >> ... >> fn` on an istringstream over `rest` (libstdc++ num_get::_M_extract_float under the
     "C" locale, model_loader.cpp:59,67,237,251,256): each extraction skips whitespace (none left: failbit, the

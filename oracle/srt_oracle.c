@@ -32,9 +32,11 @@ static inline v3 muls(v3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
 static inline v3 smul(float s, v3 a) { return V(s * a.x, s * a.y, s * a.z); }
 static inline v3 divs(v3 a, float s) { return V(a.x / s, a.y / s, a.z / s); }
 static inline v3 neg(v3 a) { return V(-a.x, -a.y, -a.z); }
-static inline float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+/* GLSL dot / cross built-ins with fused multiply-adds:
+ * dot = fma(z, z', fma(y, y', x * x')), cross_i = fma(a_j, b_k, -(a_k * b_j)). */
+static inline float dot(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 static inline v3 cross(v3 a, v3 b) {
-  return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+  return V(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
 }
 static inline float length3(v3 a) { return sqrtf(dot(a, a)); }
 static inline v3 normalize3(v3 a) { float inv = 1.0f / sqrtf(dot(a, a)); return muls(a, inv); }
@@ -192,7 +194,7 @@ typedef struct {
 
 /* raytrace_utils.glsl:28-30 */
 float oracle_rand_float(float sx, float sy) {
-  float d = sx * 12.9898f + sy * 78.233f;
+  float d = fmaf(sy, 78.233f, sx * 12.9898f);  /* dot(seed, vec2(12.9898, 78.233)) */
   float m = oracle_sin(d) * 43758.5453f;
   return fractf(m);
 }
@@ -219,7 +221,7 @@ static v3 sample_square(Ctx* c, int samp) {
 }
 
 /* raytrace_utils.glsl:107-109 */
-static inline float luminance(v3 c) { return c.x * 0.2126f + c.y * 0.7152f + c.z * 0.0722f; }
+static inline float luminance(v3 c) { return dot(c, V(0.2126f, 0.7152f, 0.0722f)); }  /* raytrace_utils.glsl:107-109 */
 /* raytrace_utils.glsl:111-113: mix(x, y, a) = x*(1-a) + y*a */
 static inline v3 specularF0(v3 base, float metal) {
   float om = 1.0f - metal;

@@ -158,7 +158,7 @@ __device__ __forceinline__ int wrap_index(int a, int m) {
 
 // raytrace_utils.glsl:28-30
 __device__ __forceinline__ float rand_float(float sx, float sy) {
-  const float d = sx * 12.9898f + sy * 78.233f;
+  const float d = __builtin_fmaf(sy, 78.233f, sx * 12.9898f);  // dot(seed, vec2(12.9898, 78.233))
   return fractf(sin_f(d) * 43758.5453f);
 }
 
@@ -174,7 +174,7 @@ __device__ __forceinline__ float randU(const KParams& kp, const Lane& ln, Counte
   return kp.noise_u[randU_index(kp, ln, sx, sy)];
 }
 
-__device__ __forceinline__ float luminance(f3 c) { return c.x * 0.2126f + c.y * 0.7152f + c.z * 0.0722f; }
+__device__ __forceinline__ float luminance(f3 c) { return dot(c, mk(0.2126f, 0.7152f, 0.0722f)); }
 __device__ __forceinline__ f3 specularF0(f3 b, float m) {
   const float om = 1.0f - m;
   return mk(0.04f * om + b.x * m, 0.04f * om + b.y * m, 0.04f * om + b.z * m);

@@ -47,9 +47,13 @@ __device__ __forceinline__ f3 operator*(f3 a, float s) { return mk(a.x * s, a.y 
 __device__ __forceinline__ f3 operator*(float s, f3 a) { return mk(s * a.x, s * a.y, s * a.z); }
 __device__ __forceinline__ f3 operator/(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
 __device__ __forceinline__ f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
-__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// GLSL dot / cross built-ins with fused multiply-adds, as GPU compilers evaluate
+// them: dot = fma(z, z', fma(y, y', x * x')),
+// cross_i = fma(a_j, b_k, -(a_k * b_j)); every other expression stays unfused.
+__device__ __forceinline__ float dot(f3 a, f3 b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {
-  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+  return mk(__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
+            __builtin_fmaf(a.x, b.y, -(a.y * b.x)));
 }
 __device__ __forceinline__ float length(f3 a) { return __builtin_sqrtf(dot(a, a)); }
 __device__ __forceinline__ f3 normalize(f3 a) {

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 from oracle import pyoracle as O
+from oracle import scene_ref as REF
 
 
 def test_sin_cos_accuracy():
@@ -68,7 +69,8 @@ def test_pow5_is_correctly_rounded():
 
 def test_rand_float_is_fract_of_scaled_sin():
     for sx, sy in ((0.0, 0.0), (1.25, -3.5), (17.0, 9.0), (-8.7238, 5.9055)):
-        d = np.float32(np.float32(sx) * np.float32(12.9898)) + np.float32(np.float32(sy) * np.float32(78.233))
+        # dot(seed, vec2(12.9898, 78.233)) under the contract: fma(sy, 78.233, sx * 12.9898)
+        d = REF.fma_f32(np.float32(sy), np.float32(78.233), np.float32(np.float32(sx) * np.float32(12.9898)))
         m = np.float32(np.float32(O.sin(float(d))) * np.float32(43758.5453))
         want = np.float32(m - np.float32(math.floor(m)))
         assert O.rand_float(sx, sy) == float(want)
