@@ -3,7 +3,7 @@
 # profiles/counters.json (tools/pmc_roofline.py <dir> --workload synthetic10000000_4096x4096_16spp).
 cd /root/repo && export TMPDIR=/tmp
 O=${O:-gpurun_out/c5pmc}; mkdir -p $O
-B="python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-global-leg --scene synthetic --width 4096 --height 4096 --spp 16"
+B="python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-global-leg --no-surface-leg --scene synthetic --width 4096 --height 4096 --spp 16"
 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT \
   SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_sq -o run -- \
   $B > $O/pmc_sq.log 2>&1 && \
