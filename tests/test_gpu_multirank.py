@@ -45,7 +45,7 @@ def _run_bench(tmp_path: pathlib.Path, world: int, band: int):
     dump = tmp_path / f"frame_w{world}_b{band}.npz"
     cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
            "--width", str(W), "--height", str(H), "--spp", str(SPP), "--band-rows", str(band),
-           "--no-cpu-baseline", "--no-global-leg", "--backend", "gloo", "--same-device", "--dump", str(dump)]
+           "--no-cpu-baseline", "--no-global-leg", "--no-surface-leg", "--backend", "gloo", "--same-device", "--dump", str(dump)]
     procs = []
     for rank in range(world):
         env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
@@ -68,7 +68,7 @@ def _run_bench(tmp_path: pathlib.Path, world: int, band: int):
         return z["accum"], z["out"], line[-1]
 
 
-@pytest.mark.parametrize("world,band", [(2, 2), (3, 8), (1, 2)])
+@pytest.mark.parametrize("world,band", [(2, 2), (3, 8), (4, 2), (1, 2)])
 def test_bench_ranks_assemble_the_one_rank_frame(tmp_path, world, band):
     import json
 
