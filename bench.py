@@ -285,8 +285,10 @@ def run_leg(setup, spp, args, *, rank, world, device, stream):
     return float(elapsed.item()), total_rays, st, kernel_ms, run
 
 
-KERNEL_LDS = "srt::sample_kernel<false, true, true, 1024, false> (LDS-resident scene)"
-KERNEL_GLOBAL = "srt::sample_kernel<false, false, true, 256, false> (global-scene mode)"
+KERNEL_LDS = "srt::sample_kernel<false, true, true, 1024, false, false> (LDS-resident scene)"
+# global-scene mode: fused sub-steps for trees under 600 MB (both legs), the IL pattern past it (C5)
+KERNEL_GLOBAL = "srt::sample_kernel<false, false, true, 256, false, true> (global-scene mode, fused sub-steps)"
+KERNEL_GLOBAL_IL = "srt::sample_kernel<false, false, true, 256, false, false> (global-scene mode, IL sub-steps)"
 
 
 def main(argv=None):
@@ -357,7 +359,8 @@ def main(argv=None):
         ms_per_step = elapsed_s * 1e3 / args.steps
         value = total_rays * args.steps / elapsed_s / 1e6
         k_ms = float(np.mean(kernel_ms))
-        kname = {"rubik": KERNEL_LDS, "synthetic": KERNEL_GLOBAL}.get(args.scene, "srt::sample_kernel<false, ...>")
+        kname = {"rubik": KERNEL_LDS, "synthetic": KERNEL_GLOBAL if args.synthetic_tris * 112 < 600 << 20
+                 else KERNEL_GLOBAL_IL}.get(args.scene, "srt::sample_kernel<false, ...>")
         line = {
             "metric": "Mrays/s (CheckHit queries: camera + bounce + shadow rays) at the BASELINE frame/spp",
             "value": round(value, 3),

@@ -44,7 +44,8 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
 // waves per SIMD the register allocation must allow: 4 (<= 128 VGPRs) in LDS
 // mode, where the 1024-thread block's LDS caps residency at 4 anyway;
 // SRT_GLOBAL_WAVES in global-scene mode, whose HBM latency wants more waves
-template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX>
+// FUSE: global-scene mode's fused sub-steps (trav_fused) instead of kStepPattern
+template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX, bool FUSE>
 __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_kernel(KParams kp) {
   const int tid = threadIdx.x;
 #ifdef SRT_WAVE_TRACE
@@ -272,7 +273,7 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
         d_leaf += __popcll(__ballot(tr.active && trav_at_leaf(tr.cnt)));
         d_int += __popcll(__ballot(tr.active && tr.cnt == 0));
 #endif
-        if (tr.active) trav_step<COUNT, LDSM, PACK>(kp, ln, c, tr, ro, rd, shadow_phase);
+        if (tr.active) trav_step<COUNT, LDSM, PACK, FUSE>(kp, ln, c, tr, ro, rd, shadow_phase);
       }
     }
 

@@ -97,6 +97,7 @@ struct srt_context {
   bool scene_ok = false;
   bool lds_ok = false;        // scene indices fit the packed LDS stack entry
   bool force_global = false;  // SRT_FORCE_GLOBAL_SCENE=1 disables LDS mode
+  bool fused = false;         // global-scene mode's fused sub-steps (set at upload: trees the Infinity Cache holds)
   // lights
   std::vector<srt_light> h_lights;
   float4* d_lights = nullptr;
@@ -314,16 +315,16 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
 // LDS budget per CU (gfx950: 160 KiB; one 1024-thread block per CU in LDS mode)
 constexpr size_t kLdsBytes = 160 * 1024;
 
-template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX>
+template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX, bool FUSE = false>
 int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
   // resident blocks per CU, queried once per (kernel instance, LDS size): the
   // query runs on the host between the launch's timing events otherwise
-  const void* fn = reinterpret_cast<const void*>(&srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX>);
+  const void* fn = reinterpret_cast<const void*>(&srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX, FUSE>);
   int per_cu = 0;
   for (const auto& e : c->occupancy)
     if (e.fn == fn && e.lds == lds) per_cu = e.per_cu;
   if (per_cu == 0) {
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX>,
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX, FUSE>,
                                                           BLOCK, lds));
     per_cu = std::max(per_cu, 1);
     c->occupancy.push_back({fn, lds, per_cu});
@@ -361,7 +362,7 @@ int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
     kp.tail_start = (int)std::max<long long>(0, n_batches - (long long)c->tail_claims * srt::kClaim * waves);
   }
   HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
-  hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX>), dim3(blocks), dim3(BLOCK), lds, c->stream, kp);
+  hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX, FUSE>), dim3(blocks), dim3(BLOCK), lds, c->stream, kp);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
   return SRT_OK;
@@ -376,6 +377,8 @@ int LaunchMode(srt_context* c, const srt::KParams& kc, size_t lds, bool count, b
   if (count) return pack ? LaunchSamples<true, false, true, 256, TEX>(c, kc, lds)
                          : LaunchSamples<true, false, false, 256, TEX>(c, kc, lds);
   if (ldsm) return LaunchSamples<false, true, true, 1024, TEX>(c, kc, lds);
+  if (c->fused) return pack ? LaunchSamples<false, false, true, 256, TEX, true>(c, kc, lds)
+                            : LaunchSamples<false, false, false, 256, TEX, true>(c, kc, lds);
   return pack ? LaunchSamples<false, false, true, 256, TEX>(c, kc, lds)
               : LaunchSamples<false, false, false, 256, TEX>(c, kc, lds);
 }
@@ -879,6 +882,14 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   const char* al_env = std::getenv("SRT_NODE_ALIGN");
   const double scene_mb = (32.0 * n_nodes + 48.0 * n_tris) / (1 << 20);
   const bool align = al_env ? al_env[0] == '1' : scene_mb >= 192.0;
+  // Global-scene traversal schedule: fused sub-steps (trav_fused: one memory
+  // round trip per step for both node kinds) while the kernel waits on latency
+  // (1 M, 101 MB: 1232 -> 1373 Mrays/s; 262 k torus knot 4576 -> 5432; 3 M,
+  // 336 MB: 832 -> 869); the IL pattern once the tree streams from HBM and
+  // the bytes bound it (10 M, 1.1 GB, at 1080p: 543 vs 528).  Crossover taken
+  // at 600 MB; SRT_GLOBAL_FUSED_MODE=1/0 forces either.
+  const char* fu_env = std::getenv("SRT_GLOBAL_FUSED_MODE");
+  c->fused = fu_env ? fu_env[0] == '1' : scene_mb < 600.0;
   bool laid = !(lay_env && lay_env[0] == '0') && LayoutNodes(nodes, n_nodes, bvhs, n_bvhs, align, &remap, &n_slots);
   if (!laid) {
     remap.resize(n_nodes);

@@ -330,6 +330,11 @@ constexpr uint32_t kNodePad = 2;          // zero node records past the array: t
 // they hide (5,676 -> 5,239 Mrays/s on Rubik 1080p).
 template <bool LDSM>
 constexpr bool kSpine = SRT_SPINE && !LDSM;
+// Global-scene mode, fused schedule (trav_fused): sub-steps per traversal iteration
+#ifndef SRT_GLOBAL_FUSED
+#define SRT_GLOBAL_FUSED 8
+#endif
+constexpr int kFusedSteps = SRT_GLOBAL_FUSED;
 static_assert(kLeafTris >= 1 && kLeafTris - 1 <= kTriPad, "kLeafTris");
 
 // Sets up BVH `t.bi` for the world ray (the reference's per-model transform,
@@ -354,14 +359,14 @@ __device__ __forceinline__ void trav_begin_bvh(const KParams& kp, Counters& c, T
 // Leaf sub-step: up to kLeafTris triangles of the current leaf, in order: each
 // is tested against the distance the previous one left; a shadow ray stops at
 // its first accept (the triangle array is padded with kTriPad zero records).
+// `tp`: the kLeafTris triangle records from t.ref on, already loaded (3 float4 each).
 template <bool COUNT, bool LDSM>
-__device__ __forceinline__ void trav_leaf(const KParams& kp, Counters& c, Trav& t, bool any) {
+__device__ __forceinline__ void trav_leaf_x(const KParams& kp, Counters& c, Trav& t, bool any, const float4* tp) {
   const uint32_t n = t.cnt < (uint32_t)kLeafTris ? t.cnt : (uint32_t)kLeafTris;
   bump<COUNT>(c, ST_TRIS, n);
   float dist = t.dist;
   uint32_t hit = t.hit;
   bool stop = false;
-  const float4* tp = tri_ptr<LDSM>(kp, t.ref);
   // all triangles' loads and reciprocals first (one shared fallback branch),
   // so the triangles' arithmetic overlaps; then the tests in order
   TriPrep pr[kLeafTris];
@@ -390,23 +395,19 @@ __device__ __forceinline__ void trav_leaf(const KParams& kp, Counters& c, Trav& 
   t.sp = stop ? 0 : t.sp;  // a stopped shadow ray pops nothing (trav_pop tests no `active`)
   if constexpr (!LDSM) t.lo = stop ? 0 : t.lo;
 }
+template <bool COUNT, bool LDSM>
+__device__ __forceinline__ void trav_leaf(const KParams& kp, Counters& c, Trav& t, bool any) {
+  trav_leaf_x<COUNT, LDSM>(kp, c, t, any, tri_ptr<LDSM>(kp, t.ref));
+}
 
 // Internal sub-step: test both children's boxes; push c0 when both pass, go to
 // c1 if it passes, else to c0 if it passes.
+// (l0, h0, l1, h1): the child pair; (m0, g0, m1, g1): c1's child pair when `spine`.
 template <bool COUNT, bool LDSM, bool PACK>
-__device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln, Counters& c, Trav& t) {
-  const uint32_t ref0 = t.ref | kp.ref_or;  // the child pair's first slot
-  const bool spine = kSpine<LDSM> && (ref0 != t.ref);  // c1 is internal and its pair follows
-  const uint32_t pi = 2 * ref0 + 2;
-  const float4 l0 = node4<LDSM>(kp, pi), h0 = node4<LDSM>(kp, pi + 1);
-  const float4 l1 = node4<LDSM>(kp, pi + 2), h1 = node4<LDSM>(kp, pi + 3);
-  float4 m0, g0, m1, g1;  // c1's child pair
-  if (spine) {
-    m0 = node4<LDSM>(kp, pi + 4);
-    g0 = node4<LDSM>(kp, pi + 5);
-    m1 = node4<LDSM>(kp, pi + 6);
-    g1 = node4<LDSM>(kp, pi + 7);
-  }
+__device__ __forceinline__ void trav_internal_x(const KParams& kp, const Lane& ln, Counters& c, Trav& t,
+                                                const float4 l0, const float4 h0, const float4 l1, const float4 h1,
+                                                const float4 m0, const float4 g0, const float4 m1, const float4 g1,
+                                                const bool spine) {
   bump<COUNT>(c, ST_NODES, 2);
   float b0, b1;
   const bool v0 = box_test(t.o, t.inv, l0, h0, t.dist, b0);
@@ -456,6 +457,60 @@ __device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln,
     }
   }
 }
+template <bool COUNT, bool LDSM, bool PACK>
+__device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln, Counters& c, Trav& t) {
+  const uint32_t ref0 = t.ref | kp.ref_or;  // the child pair's first slot
+  const bool spine = kSpine<LDSM> && (ref0 != t.ref);  // c1 is internal and its pair follows
+  const uint32_t pi = 2 * ref0 + 2;
+  const float4 l0 = node4<LDSM>(kp, pi), h0 = node4<LDSM>(kp, pi + 1);
+  const float4 l1 = node4<LDSM>(kp, pi + 2), h1 = node4<LDSM>(kp, pi + 3);
+  float4 m0, g0, m1, g1;  // c1's child pair
+  if (spine) {
+    m0 = node4<LDSM>(kp, pi + 4);
+    g0 = node4<LDSM>(kp, pi + 5);
+    m1 = node4<LDSM>(kp, pi + 6);
+    g1 = node4<LDSM>(kp, pi + 7);
+  }
+  trav_internal_x<COUNT, LDSM, PACK>(kp, ln, c, t, l0, h0, l1, h1, m0, g0, m1, g1, spine);
+}
+
+template <bool LDSM, bool PACK>
+__device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav& t);
+
+// Global-scene mode: one sub-step for both node kinds.  Lanes at an internal
+// node and lanes at a leaf issue their loads (node pairs or triangle records)
+// as one set of per-lane-addressed loads, so the wave waits for memory once
+// for both; then each kind's tests run on their lanes.  The memory-latency-bound
+// global mode trades the second kind's idle lanes for half the round trips;
+// each lane's steps, and so its decisions, are unchanged.
+template <bool COUNT, bool PACK>
+__device__ __forceinline__ void trav_fused(const KParams& kp, const Lane& ln, Counters& c, Trav& t, bool any) {
+  const bool at_int = t.cnt == 0u, at_leaf = trav_at_leaf(t.cnt);
+  if (at_int | at_leaf) {
+    const uint32_t ref0 = t.ref | kp.ref_or;
+    const bool spine = kSpine<false> && at_int && (ref0 != t.ref);
+    // leaf: kLeafTris = 2 records (6 float4; kTriPad zero records keep them in
+    // bounds); internal: the pair (4 float4) and, on the spine, the next pair
+    static_assert(kLeafTris == 2, "trav_fused loads two triangle records");
+    const float4* p = at_leaf ? kp.tris + 3 * (size_t)t.ref : kp.nodes + (2 * ref0 + 2);
+    float4 x[8];
+    x[0] = p[0];
+    x[1] = p[1];
+    x[2] = p[2];
+    x[3] = p[3];
+    if (at_leaf | spine) {
+      x[4] = p[4];
+      x[5] = p[5];
+    }
+    if (spine) {
+      x[6] = p[6];
+      x[7] = p[7];
+    }
+    if (at_int) trav_internal_x<COUNT, false, PACK>(kp, ln, c, t, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], spine);
+    else trav_leaf_x<COUNT, false>(kp, c, t, any, x);
+  }
+  trav_pop<false, PACK>(kp, ln, t);
+}
 
 // Nothing current: pop one entry (visited if it still beats the running
 // distance).  A lane whose stack is empty waits for trav_finish at the end of
@@ -498,9 +553,15 @@ __device__ __forceinline__ void trav_finish(const KParams& kp, Trav& t, bool any
   }
 }
 
-template <bool COUNT, bool LDSM, bool PACK, int K>
+template <bool COUNT, bool LDSM, bool PACK, bool FUSE, int K>
 __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln, Counters& c, Trav& t, bool any) {
-  if constexpr (kStepPattern[K] != 0) {
+  if constexpr (FUSE) {
+    static_assert(!LDSM, "fused sub-steps are a global-scene mode schedule");
+    if constexpr (K < kFusedSteps) {
+      trav_fused<COUNT, PACK>(kp, ln, c, t, any);
+      trav_substeps<COUNT, LDSM, PACK, FUSE, K + 1>(kp, ln, c, t, any);
+    }
+  } else if constexpr (kStepPattern[K] != 0) {
     if constexpr (kStepPattern[K] == 'I') {
       DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K, t.cnt == 0);
       if (t.cnt == 0) trav_internal<COUNT, LDSM, PACK>(kp, ln, c, t);
@@ -510,7 +571,7 @@ __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln,
     }
     DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K + 2, t.active & (t.cnt == kNoneCnt));
     trav_pop<LDSM, PACK>(kp, ln, t);
-    trav_substeps<COUNT, LDSM, PACK, K + 1>(kp, ln, c, t, any);
+    trav_substeps<COUNT, LDSM, PACK, FUSE, K + 1>(kp, ln, c, t, any);
   }
 }
 
@@ -519,11 +580,11 @@ __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln,
 // node is of its kind, so a lane makes up to strlen(kStepPattern) steps of
 // its own sequence per iteration, in order.  `any` selects the shadow-ray
 // (first hit) variant.
-template <bool COUNT, bool LDSM, bool PACK>
+template <bool COUNT, bool LDSM, bool PACK, bool FUSE>
 __device__ __forceinline__ void trav_step(const KParams& kp, const Lane& ln, Counters& c, Trav& t, f3 ro, f3 rd,
                                           bool any) {
   if (t.start) trav_begin_bvh<COUNT, LDSM>(kp, c, t, ro, rd);  // only for BVHs after the first
-  trav_substeps<COUNT, LDSM, PACK, 0>(kp, ln, c, t, any);
+  trav_substeps<COUNT, LDSM, PACK, FUSE, 0>(kp, ln, c, t, any);
   trav_finish(kp, t, any);
 }
 

@@ -195,11 +195,16 @@ def test_surface_mesh_global_mode():
     assert_parity(setup, 2)
 
 
-@pytest.mark.parametrize("env", [{"SRT_NODE_ALIGN": "1"}, {"SRT_NODE_LAYOUT": "0"}])
+@pytest.mark.parametrize("env", [{"SRT_NODE_ALIGN": "1"}, {"SRT_NODE_LAYOUT": "0"},
+                                 {"SRT_NODE_ALIGN": "1", "SRT_GLOBAL_FUSED_MODE": "1"},
+                                 {"SRT_NODE_ALIGN": "0", "SRT_GLOBAL_FUSED_MODE": "0"},
+                                 {"SRT_NODE_LAYOUT": "0", "SRT_GLOBAL_FUSED_MODE": "1"}])
 def test_node_layouts_global_mode(monkeypatch, env):
     """The device node layouts (pathtrace.hip LayoutNodes): line-aligned right-child chains (chosen for
     scenes past the Infinity Cache) and the reference's own order (no right-spine double steps) render
-    the oracle's frame in global-scene mode, two models with a moved second one included."""
+    the oracle's frame in global-scene mode, two models with a moved second one included; so do both
+    traversal schedules (fused sub-steps, chosen with the dense layout, and the IL pattern) on
+    every layout."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     setup = R.make_setup(48, 40, show_model=True, models=[R.synthetic_model(30000, seed=3)])

@@ -1,7 +1,8 @@
 """Writes profiles/counters.json from a round's rocprofv3 PMC passes (tools/profile_round.sh).
 
 usage: python tools/pmc_roofline.py gpurun_out/r02 [--tag r02] [--workload NAME]
-(--workload: a single-leg run, e.g. tools/pmc_c5.sh's, whose global-scene instance is NAME)
+(--workload: a single-leg run, e.g. tools/pmc_c5.sh's, whose global-scene instance is NAME; --il: that
+run took the IL-pattern instance, as trees past 600 MB do)
 
 Each pass ran `python bench.py --steps 1 --warmup 0 --no-cpu-baseline`, so every leg's timed step
 launched its sample_kernel<false, ...> instance exactly once (the counting run is the <true, ...>
@@ -23,14 +24,14 @@ only = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv el
 root = pathlib.Path(__file__).resolve().parent.parent
 
 LEGS = {  # kernel instance -> the workloads bench.py runs on it, in launch order (one timed launch each)
-    "void srt::sample_kernel<false, true, true, 1024, false>": ["rubik_1920x1080_256spp"],
-    "void srt::sample_kernel<false, false, true, 256, false>": ["synthetic1000000_1920x1080_16spp",
+    "void srt::sample_kernel<false, true, true, 1024, false, false>": ["rubik_1920x1080_256spp"],
+    "void srt::sample_kernel<false, false, true, 256, false, true>": ["synthetic1000000_1920x1080_16spp",
                                                                 "torusknot262144_1920x1080_64spp"],
 }
 
 
 if only:
-    LEGS = {"void srt::sample_kernel<false, false, true, 256, false>": [only]}
+    LEGS = {"void srt::sample_kernel<false, false, true, 256, false, " + ("false>" if "--il" in sys.argv else "true>"): [only]}
 
 
 def rows(sub):
