@@ -39,6 +39,7 @@ struct KParams {
   int ext_w, ext_h;
   int stack_entries;
   int nodes_f4, tris_f4;   // LDS-resident scene: sizes of the node / triangle arrays in float4
+  int nodes_lds_f4;        // LDS mode: float4 the node copy occupies (pair blocks padded, traversal.hpp node_lds_f4)
   // internal nodes' child index: pairs start at odd slots and an even index (the
   // pair's start - 1) flags a right child whose own pair follows (pathtrace.hip
   // LayoutNodes); ref_or = 1 decodes it, 0 for the identity layout (no flags)

@@ -53,9 +53,9 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
   unsigned long long tw2 = 0;
 #endif
   if constexpr (LDSM) {  // the block copies the scene (nodes + triangles) into LDS once
-    const int total = kp.nodes_f4 + kp.tris_f4;
-    for (int i = tid; i < total; i += blockDim.x)
-      g_smem[i] = (i < kp.nodes_f4) ? kp.nodes[i] : kp.tris[i - kp.nodes_f4];
+    // (node pair blocks at the padded stride, node_lds_f4; the pad slots are never read)
+    for (int i = tid; i < kp.nodes_f4; i += blockDim.x) g_smem[node_lds_f4((uint32_t)i)] = kp.nodes[i];
+    for (int i = tid; i < kp.tris_f4; i += blockDim.x) g_smem[kp.nodes_lds_f4 + i] = kp.tris[i];
   }
   {  // and the light and material records, when they fit (shading reads them from LDS)
     const int nl = kp.lights_lds ? 2 * (kp.light_records + 1) : 0, nm = kp.mats_lds ? 2 * kp.mat_records : 0;

@@ -96,6 +96,7 @@ struct srt_context {
   int stack_entries = 1;
   bool scene_ok = false;
   bool lds_ok = false;        // scene indices fit the packed LDS stack entry
+  bool pairs_aligned = false; // every internal node's child pair starts at an odd slot (LDS mode's node_pair)
   bool force_global = false;  // SRT_FORCE_GLOBAL_SCENE=1 disables LDS mode
   bool fused = false;         // global-scene mode's fused sub-steps (set at upload: trees the Infinity Cache holds)
   // lights
@@ -306,6 +307,7 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
   kp->ext_h = c->H;
   kp->stack_entries = c->stack_entries;
   kp->nodes_f4 = (int)(2 * ((size_t)c->n_nodes + 1));
+  kp->nodes_lds_f4 = (int)((((size_t)kp->nodes_f4 + 3) >> 2) * srt::kNodeBlkF4);  // padded pair blocks
   kp->ref_or = c->ref_or;
   kp->tris_f4 = (int)(3 * ((size_t)c->n_tris + srt::kTriPad));  // with the padding records
   CameraParams(c, kp);
@@ -396,13 +398,14 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   }
   if (kp.nframes <= 0) return SRT_OK;
   // LDS mode: the whole scene + 1024 lanes' 2-dword stacks fit in one CU's LDS
-  const size_t scene_bytes = ((size_t)kp.nodes_f4 + (size_t)kp.tris_f4) * sizeof(float4);
+  // (node pairs at the padded LDS stride; only for node arrays whose pairs are all 64-B aligned)
+  const size_t scene_bytes = ((size_t)kp.nodes_lds_f4 + (size_t)kp.tris_f4) * sizeof(float4);
   const size_t lds_mode_bytes = scene_bytes + (size_t)1024 * 2 * sizeof(uint32_t) * (size_t)kp.stack_entries;
-  const bool ldsm = kp.show_model && c->lds_ok && !c->force_global && lds_mode_bytes <= kLdsBytes;
+  const bool ldsm = kp.show_model && c->lds_ok && c->pairs_aligned && !c->force_global && lds_mode_bytes <= kLdsBytes;
   const int block = ldsm ? 1024 : 256;
   size_t lds;
   if (ldsm) {
-    kp.stack_base_f4 = kp.nodes_f4 + kp.tris_f4;
+    kp.stack_base_f4 = kp.nodes_lds_f4 + kp.tris_f4;
     lds = lds_mode_bytes;
   } else {  // LDS rings of kShortStack entries per lane, backed by HBM stacks (LaunchSamples)
     kp.stack_base_f4 = 0;
@@ -897,6 +900,7 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
     n_slots = n_nodes;
   }
   std::vector<float4> hn(2 * ((size_t)n_slots + 1 + srt::kNodePad), make_float4(0, 0, 0, 0));
+  bool pairs_aligned = true;
   for (uint32_t i = 0; i < n_nodes; ++i) {
     if (remap[i] == 0xFFFFFFFFu) continue;
     const srt_bvh_node& n = nodes[i];
@@ -904,6 +908,7 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
     if (n.prim_count == 0) {  // internal: c0's slot, less 1 when c1 is internal (its pair then follows)
       first = remap[first];
       if (laid && nodes[n.first_child_or_prim_index + 1].prim_count == 0) first -= 1;
+      if (((first | (laid ? 1u : 0u)) & 1u) == 0) pairs_aligned = false;  // overlapping sibling pairs
     }
     float w0, w1;
     std::memcpy(&w0, &first, 4);
@@ -991,6 +996,7 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   uint32_t max_leaf = 0;
   for (uint32_t i = 0; i < n_nodes; ++i) max_leaf = std::max(max_leaf, nodes[i].prim_count);
   c->lds_ok = n_tris < (1u << 24) && n_slots + srt::kNodePad < (1u << 24) && max_leaf < 256;
+  c->pairs_aligned = pairs_aligned;
   c->scene_ok = true;
   if (c->bvh_count == 0) c->bvh_count = n_bvhs;
   // the zero records beyond n_bvhs traverse from node 0 with a zero ray

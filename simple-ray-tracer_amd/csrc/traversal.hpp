@@ -46,22 +46,51 @@ __device__ __forceinline__ bool box_test(f3 o, f3 inv, float4 lo, float4 hi, flo
 __device__ __forceinline__ float4 lds4(uint32_t byte_off) {
   return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(g_smem) + byte_off);
 }
+// LDS mode stores the node array's 64-B sibling-pair blocks (float4 4b .. 4b + 3)
+// at a stride of kNodeBlkF4 float4.  A ds_read_b128 serves 16 lanes per LDS
+// cycle from a 256-B bank row (16 slots of 16 B); with 64-B blocks every lane
+// reading field k of some pair lands on one of only 4 slots, (4 * pair + k) mod 16,
+// so random pairs collide ~4 ways.  An 80-B stride spreads them over all 16.
+#ifndef SRT_NODE_PAD
+#define SRT_NODE_PAD 1
+#endif
+constexpr uint32_t kNodeBlkF4 = SRT_NODE_PAD ? 5u : 4u;
+__device__ __forceinline__ uint32_t node_lds_f4(uint32_t i) { return (i >> 2) * kNodeBlkF4 + (i & 3u); }
 template <bool LDSM>
 __device__ __forceinline__ float4 node4(const KParams& kp, uint32_t i) {
-  if constexpr (LDSM) return lds4(i << 4);
+  if constexpr (LDSM) return lds4(node_lds_f4(i) << 4);
   else return kp.nodes[i];
+}
+// The child pair whose first slot is `ref0` (odd: the pair's block is 64-B
+// aligned; LDS mode is only chosen for node arrays where every pair is).
+template <bool LDSM>
+__device__ __forceinline__ void node_pair(const KParams& kp, uint32_t ref0, float4& l0, float4& h0, float4& l1,
+                                          float4& h1) {
+  if constexpr (LDSM) {
+    const uint32_t b = ((ref0 + 1u) >> 1) * (kNodeBlkF4 * 16u);
+    l0 = lds4(b);
+    h0 = lds4(b + 16u);
+    l1 = lds4(b + 32u);
+    h1 = lds4(b + 48u);
+  } else {
+    const uint32_t pi = 2 * ref0 + 2;
+    l0 = kp.nodes[pi];
+    h0 = kp.nodes[pi + 1];
+    l1 = kp.nodes[pi + 2];
+    h1 = kp.nodes[pi + 3];
+  }
 }
 // the records of triangle `i` onwards (3 float4 per triangle)
 template <bool LDSM>
 __device__ __forceinline__ const float4* tri_ptr(const KParams& kp, uint32_t i) {
   if constexpr (LDSM)  // i < 2^24 in LDS mode: one v_mad_u32_u24 (a 32-bit mul + add becomes a slow v_mad_u64_u32)
-    return reinterpret_cast<const float4*>(reinterpret_cast<const char*>(g_smem) + ((uint32_t)kp.nodes_f4 * 16u +
+    return reinterpret_cast<const float4*>(reinterpret_cast<const char*>(g_smem) + ((uint32_t)kp.nodes_lds_f4 * 16u +
                                                                                   __umul24(i, 48u)));
   else return kp.tris + 3 * (size_t)i;
 }
 template <bool LDSM>
 __device__ __forceinline__ float4 tri4(const KParams& kp, uint32_t i) {
-  if constexpr (LDSM) return lds4(((uint32_t)kp.nodes_f4 + i) << 4);
+  if constexpr (LDSM) return lds4(((uint32_t)kp.nodes_lds_f4 + i) << 4);
   else return kp.tris[i];
 }
 
@@ -462,8 +491,8 @@ __device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln,
   const uint32_t ref0 = t.ref | kp.ref_or;  // the child pair's first slot
   const bool spine = kSpine<LDSM> && (ref0 != t.ref);  // c1 is internal and its pair follows
   const uint32_t pi = 2 * ref0 + 2;
-  const float4 l0 = node4<LDSM>(kp, pi), h0 = node4<LDSM>(kp, pi + 1);
-  const float4 l1 = node4<LDSM>(kp, pi + 2), h1 = node4<LDSM>(kp, pi + 3);
+  float4 l0, h0, l1, h1;
+  node_pair<LDSM>(kp, ref0, l0, h0, l1, h1);
   float4 m0, g0, m1, g1;  // c1's child pair
   if (spine) {
     m0 = node4<LDSM>(kp, pi + 4);
