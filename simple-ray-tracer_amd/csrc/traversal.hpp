@@ -67,7 +67,10 @@ template <bool LDSM>
 __device__ __forceinline__ void node_pair(const KParams& kp, uint32_t ref0, float4& l0, float4& h0, float4& l1,
                                           float4& h1) {
   if constexpr (LDSM) {
-    const uint32_t b = ((ref0 + 1u) >> 1) * (kNodeBlkF4 * 16u);
+    // block (ref0 + 1) / 2 = ref0 / 2 + 1 (ref0 is odd), of 16 * kNodeBlkF4 bytes; ref0 < 2^24 in LDS
+    // mode, so a v_mad_u32_u24 (a 32-bit multiply is a quarter-rate v_mul_lo_u32), and the
+    // compiler sees the 16-B alignment that lets it use ds_read_b128
+    const uint32_t b = __umul24(ref0 >> 1, kNodeBlkF4 * 16u) + kNodeBlkF4 * 16u;
     l0 = lds4(b);
     h0 = lds4(b + 16u);
     l1 = lds4(b + 32u);
