@@ -129,6 +129,7 @@ struct srt_context {
   size_t lbuf_cap = (size_t)16 << 30;  // SRT_SAMPLE_BUFFER_MB
   int tail_claims = 16;  // SRT_TAIL_CLAIMS: claims per wave before the end from which claims take one batch
   int trav_frac16 = 9;                 // SRT_TRAV_FRAC16 (measured best on Rubik 1080p with the 16-sub-step pattern)
+  int trav_frac16_global = 9;          // SRT_TRAV_FRAC16_GLOBAL: the same threshold for global-scene mode
   int num_cus = 256;
   // stats
   unsigned long long* d_stats = nullptr;
@@ -444,7 +445,7 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
     c->lbuf_bytes = need;
   }
   kp.lbuf = c->d_lbuf;
-  kp.trav_frac16 = c->trav_frac16;
+  kp.trav_frac16 = ldsm ? c->trav_frac16 : c->trav_frac16_global;
   HIP_OK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_TOTAL, c->stream));
   const int out_frames = kp.frame_first + kp.nframes - 1;
   const int nchunks = (kp.nframes + chunk - 1) / chunk;
@@ -643,6 +644,8 @@ int srt_create(int device, void* stream, srt_context** out) {
   if (const char* e = std::getenv("SRT_TAIL_CLAIMS")) c->tail_claims = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("SRT_TILE_ORDER")) c->tile_schedule = e[0] != '0';
   if (const char* e = std::getenv("SRT_TRAV_FRAC16")) c->trav_frac16 = std::max(0, std::min(16, std::atoi(e)));
+  if (const char* e = std::getenv("SRT_TRAV_FRAC16_GLOBAL"))
+    c->trav_frac16_global = std::max(0, std::min(16, std::atoi(e)));
   {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
