@@ -217,6 +217,39 @@ def test_node_layouts_global_mode(monkeypatch, env):
     assert_parity(two, 2)
 
 
+@pytest.mark.parametrize("layout", ["1", "0"])
+def test_lds_mode_node_orders(rubik, monkeypatch, layout):
+    """LDS mode reads node pairs from 80-B blocks (traversal.hpp node_pair) in both device orders: the
+    traversal-order layout and the reference's own order (SRT_NODE_LAYOUT=0, no child-index flags)."""
+    monkeypatch.setenv("SRT_NODE_LAYOUT", layout)
+    assert_parity(R.make_setup(56, 40, show_model=True, models=[rubik]), 2)
+
+
+@pytest.mark.parametrize("layout", ["1", "0"])
+def test_overlapping_sibling_pairs(rubik, monkeypatch, layout):
+    """A node array whose child pairs start at even slots (a zero node inserted after the root shifts every
+    pair by one).  Laid out again it takes LDS mode; kept in its own order (SRT_NODE_LAYOUT=0) its pairs are
+    not 64-B blocks, so the scene is traversed in global-scene mode.  Both render the oracle's frame."""
+    import dataclasses
+
+    monkeypatch.setenv("SRT_NODE_LAYOUT", layout)
+    setup = R.make_setup(48, 40, show_model=True, models=[rubik])
+    n = setup.scene.nodes
+    m = np.zeros(len(n) + 1, dtype=n.dtype)
+    m[0] = n[0]
+    m[2:] = n[1:]
+    internal = m["count"] == 0
+    internal[1] = False  # the inserted zero record is unreachable
+    m["first"][internal] += 1
+    assert (m["first"][internal] % 2 == 0).all()
+    bvhs = setup.scene.bvhs.copy()
+    assert (bvhs["first_index"] == 0).all()
+    shifted = dataclasses.replace(setup, scene=dataclasses.replace(setup.scene, nodes=m, bvhs=bvhs))
+    a, o = assert_parity(shifted, 2)
+    b, p, _ = gpu_render(setup, 2)
+    assert bits_equal(a, b).all() and (o == p).all()
+
+
 def test_lds_and_global_modes_agree(rubik, monkeypatch):
     setup = R.make_setup(64, 48, show_model=True, models=[rubik])
     a, o, _ = gpu_render(setup, 3)
