@@ -2,7 +2,8 @@
 
 usage: python tools/pmc_roofline.py gpurun_out/r02 [--tag r02] [--workload NAME]
 (--workload: a single-leg run, e.g. tools/pmc_c5.sh's, whose global-scene instance is NAME; --il: that
-run took the IL-pattern instance, as trees past 600 MB do)
+run took the IL-pattern instance, as trees past 600 MB do; --sum: sum every non-counting sample_kernel
+dispatch of a single-workload run, whatever its instance, e.g. tools/pmc_configs.sh's C2 and C4)
 
 Each pass ran `python bench.py --steps 1 --warmup 0 --no-cpu-baseline`, so every leg's timed step
 launched its sample_kernel<false, ...> instance exactly once (the counting run is the <true, ...>
@@ -32,6 +33,13 @@ LEGS = {  # kernel instance -> the workloads bench.py runs on it, in launch orde
 
 if only:
     LEGS = {"void srt::sample_kernel<false, false, true, 256, false, " + ("false>" if "--il" in sys.argv else "true>"): [only]}
+# --sum: a single-workload run whose timed step may be several launches (sample-buffer chunks, e.g. C4):
+# the counters of every non-counting sample_kernel dispatch are summed (bench's kernel_ms sums the same
+# launches' HIP-event times); the counting run is the <true, ...> instance and is left out.
+SUM = "--sum" in sys.argv
+if SUM:
+    assert only, "--sum needs --workload"
+    LEGS = {"void srt::sample_kernel<false, ": [only]}
 
 
 def rows(sub):
@@ -44,6 +52,12 @@ def per_launch(sub):
     out = {}
     for leg_kernel, wls in LEGS.items():
         rs = [r for r in rows(sub) if r["Kernel_Name"].startswith(leg_kernel)]
+        if SUM:
+            agg = {}
+            for r in rs:
+                agg[r["Counter_Name"]] = agg.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+            out[wls[0]] = agg
+            continue
         ids = sorted({int(r["Dispatch_Id"]) for r in rs})
         for wl, did in zip(wls, ids[-len(wls):] if len(ids) >= len(wls) else ids):
             agg = {}
