@@ -250,6 +250,15 @@ def test_overlapping_sibling_pairs(rubik, monkeypatch, layout):
     assert bits_equal(a, b).all() and (o == p).all()
 
 
+@pytest.mark.parametrize("n_tris", [600, 700])
+def test_lds_budget_boundary(n_tris):
+    """Meshes on either side of the LDS budget: 600 triangles (depth 11) is the fullest LDS-resident copy,
+    nodes at the 80-B pair stride + triangles + 1024 lanes' stacks = 157,248 of 163,840 bytes; 700 (depth 12)
+    no longer fits and is traversed in global-scene mode.  Both render the oracle's frame."""
+    setup = R.make_setup(48, 40, show_model=True, models=[R.synthetic_model(n_tris, seed=5)])
+    assert_parity(setup, 2)
+
+
 def test_lds_and_global_modes_agree(rubik, monkeypatch):
     setup = R.make_setup(64, 48, show_model=True, models=[rubik])
     a, o, _ = gpu_render(setup, 3)
