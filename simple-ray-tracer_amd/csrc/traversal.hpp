@@ -332,13 +332,26 @@ __device__ __forceinline__ bool trav_at_leaf(uint32_t cnt) { return (int)cnt > 0
 #ifndef SRT_LEAF_TRIS
 #define SRT_LEAF_TRIS 2
 #endif
-constexpr int kLeafTris = SRT_LEAF_TRIS;  // triangles tested per leaf step
+constexpr int kLeafTris = SRT_LEAF_TRIS;  // triangles tested per leaf step (global-scene mode)
+// LDS mode tests three triangles per leaf step, over 10 sub-steps per iteration
+// (Rubik 1080p: 5,976 -> 6,106 Mrays/s; 4 per step 5,451-5,493)
+#ifndef SRT_LEAF_TRIS_LDS
+#define SRT_LEAF_TRIS_LDS 3
+#endif
+template <bool LDSM>
+constexpr int kLeafTrisM = LDSM ? SRT_LEAF_TRIS_LDS : kLeafTris;
 // Sub-steps of one traversal iteration: 'I' expands an internal node, 'L'
 // tests a leaf's next triangles; each is followed by a pop if nothing is current.
 #ifndef SRT_STEP_PATTERN
 #define SRT_STEP_PATTERN "ILILILILILILILIL"
 #endif
-constexpr char kStepPattern[] = SRT_STEP_PATTERN;
+#ifndef SRT_STEP_PATTERN_LDS
+#define SRT_STEP_PATTERN_LDS "ILILILILIL"
+#endif
+constexpr char kStepPattern[] = SRT_STEP_PATTERN;         // global-scene mode, IL schedule
+constexpr char kStepPatternLds[] = SRT_STEP_PATTERN_LDS;  // LDS mode
+template <bool LDSM>
+constexpr char step_kind(int k) { return LDSM ? kStepPatternLds[k] : kStepPattern[k]; }
 // global-scene mode: entries per lane kept in the LDS ring (power of two)
 #ifndef SRT_SHORT_STACK
 #define SRT_SHORT_STACK 16
@@ -368,6 +381,7 @@ constexpr bool kSpine = SRT_SPINE && !LDSM;
 #endif
 constexpr int kFusedSteps = SRT_GLOBAL_FUSED;
 static_assert(kLeafTris >= 1 && kLeafTris - 1 <= kTriPad, "kLeafTris");
+static_assert(SRT_LEAF_TRIS_LDS >= 1 && SRT_LEAF_TRIS_LDS - 1 <= kTriPad, "SRT_LEAF_TRIS_LDS");
 
 // Sets up BVH `t.bi` for the world ray (the reference's per-model transform,
 // raytrace_compute.glsl:146-147) and tests its root box.
@@ -394,23 +408,24 @@ __device__ __forceinline__ void trav_begin_bvh(const KParams& kp, Counters& c, T
 // `tp`: the kLeafTris triangle records from t.ref on, already loaded (3 float4 each).
 template <bool COUNT, bool LDSM>
 __device__ __forceinline__ void trav_leaf_x(const KParams& kp, Counters& c, Trav& t, bool any, const float4* tp) {
-  const uint32_t n = t.cnt < (uint32_t)kLeafTris ? t.cnt : (uint32_t)kLeafTris;
+  constexpr int kLT = kLeafTrisM<LDSM>;
+  const uint32_t n = t.cnt < (uint32_t)kLT ? t.cnt : (uint32_t)kLT;
   bump<COUNT>(c, ST_TRIS, n);
   float dist = t.dist;
   uint32_t hit = t.hit;
   bool stop = false;
   // all triangles' loads and reciprocals first (one shared fallback branch),
   // so the triangles' arithmetic overlaps; then the tests in order
-  TriPrep pr[kLeafTris];
+  TriPrep pr[kLT];
   bool slow = false;
 #pragma unroll
-  for (int k = 0; k < kLeafTris; ++k) slow |= tri_prep(t.d, tp[3 * k], tp[3 * k + 1], tp[3 * k + 2], pr[k]);
+  for (int k = 0; k < kLT; ++k) slow |= tri_prep(t.d, tp[3 * k], tp[3 * k + 1], tp[3 * k + 2], pr[k]);
   if (__builtin_expect(slow, 0)) {
 #pragma unroll
-    for (int k = 0; k < kLeafTris; ++k) pr[k].f = 1.0f / pr[k].a;
+    for (int k = 0; k < kLT; ++k) pr[k].f = 1.0f / pr[k].a;
   }
 #pragma unroll
-  for (int k = 0; k < kLeafTris; ++k) {
+  for (int k = 0; k < kLT; ++k) {
     float tk;
     const bool tk_ok = tri_finish(t.o, t.d, pr[k], dist, tk);
     const bool ak = k == 0 ? tk_ok : (((uint32_t)k < n) & !stop & tk_ok);  // a leaf holds >= 1 triangle
@@ -593,8 +608,8 @@ __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln,
       trav_fused<COUNT, PACK>(kp, ln, c, t, any);
       trav_substeps<COUNT, LDSM, PACK, FUSE, K + 1>(kp, ln, c, t, any);
     }
-  } else if constexpr (kStepPattern[K] != 0) {
-    if constexpr (kStepPattern[K] == 'I') {
+  } else if constexpr (step_kind<LDSM>(K) != 0) {
+    if constexpr (step_kind<LDSM>(K) == 'I') {
       DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K, t.cnt == 0);
       if (t.cnt == 0) trav_internal<COUNT, LDSM, PACK>(kp, ln, c, t);
     } else {
@@ -608,8 +623,8 @@ __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln,
 }
 
 // One traversal iteration (see traverse() for the order argument): the
-// sub-steps of kStepPattern in turn, each taken by the lanes whose current
-// node is of its kind, so a lane makes up to strlen(kStepPattern) steps of
+// sub-steps of the mode's pattern in turn, each taken by the lanes whose current
+// node is of its kind, so a lane makes up to strlen(pattern) steps of
 // its own sequence per iteration, in order.  `any` selects the shadow-ray
 // (first hit) variant.
 template <bool COUNT, bool LDSM, bool PACK, bool FUSE>
