@@ -333,8 +333,9 @@ __device__ __forceinline__ bool trav_at_leaf(uint32_t cnt) { return (int)cnt > 0
 #define SRT_LEAF_TRIS 2
 #endif
 constexpr int kLeafTris = SRT_LEAF_TRIS;  // triangles tested per leaf step (global-scene mode)
-// LDS mode tests three triangles per leaf step, over 10 sub-steps per iteration
-// (Rubik 1080p: 5,976 -> 6,106 Mrays/s; 4 per step 5,451-5,493)
+// LDS mode tests three triangles per leaf step, over 11 sub-steps per iteration
+// that start with two internal steps (Rubik 1080p: 5,976 -> 6,106 Mrays/s with
+// ILIL..., 6,150-6,157 with IIL...; 4 per step 5,451-5,493)
 #ifndef SRT_LEAF_TRIS_LDS
 #define SRT_LEAF_TRIS_LDS 3
 #endif
@@ -346,7 +347,7 @@ constexpr int kLeafTrisM = LDSM ? SRT_LEAF_TRIS_LDS : kLeafTris;
 #define SRT_STEP_PATTERN "ILILILILILILILIL"
 #endif
 #ifndef SRT_STEP_PATTERN_LDS
-#define SRT_STEP_PATTERN_LDS "ILILILILIL"
+#define SRT_STEP_PATTERN_LDS "IILILILILIL"
 #endif
 constexpr char kStepPattern[] = SRT_STEP_PATTERN;         // global-scene mode, IL schedule
 constexpr char kStepPatternLds[] = SRT_STEP_PATTERN_LDS;  // LDS mode
