@@ -343,10 +343,11 @@ template <bool LDSM>
 constexpr int kLeafTrisM = LDSM ? SRT_LEAF_TRIS_LDS : kLeafTris;
 // Sub-steps of one traversal iteration: 'I' expands an internal node, 'L'
 // tests a leaf's next triangles; each is followed by a pop if nothing is current.
-// (global-scene mode's IL schedule, the one trees past 600 MB take: two internal
-// steps first, as in LDS mode; C5 582 -> 592 Mrays/s)
+// (global-scene mode's IL schedule, the one trees past 600 MB take: internal
+// steps first, as in LDS mode; C5 582 -> 592 Mrays/s with two, 594 -> 601 with
+// three)
 #ifndef SRT_STEP_PATTERN
-#define SRT_STEP_PATTERN "IILILILILILIL"
+#define SRT_STEP_PATTERN "IIILILILILILIL"
 #endif
 #ifndef SRT_STEP_PATTERN_LDS
 #define SRT_STEP_PATTERN_LDS "IILILILILIL"
