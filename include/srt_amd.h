@@ -18,7 +18,7 @@
 extern "C" {
 #endif
 
-#define SRT_ABI_VERSION 1
+#define SRT_ABI_VERSION 2  /* 2: srt_stats.bounce_cap */
 
 /* ---- status codes ---- */
 enum {
@@ -58,8 +58,9 @@ typedef struct {
   uint64_t light_reads; /* light records (32 B) */
   uint64_t mat_reads;   /* mesh material fetches (48 B) */
   uint64_t samples;     /* path samples */
-  uint64_t stack_overflow;
-  uint64_t max_stack;
+  uint64_t stack_overflow; /* traversal stack overflows (cannot happen for a BVH srt_upload_scene accepted) */
+  uint64_t max_stack;      /* deepest traversal stack */
+  uint64_t bounce_cap;     /* paths cut after 2^20 bounces (the reference's loop has no cap; env SRT_BOUNCE_CAP) */
 } srt_stats;
 
 typedef struct srt_context srt_context;

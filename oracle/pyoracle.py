@@ -15,7 +15,24 @@ import subprocess
 import numpy as np
 
 ORACLE_DIR = pathlib.Path(__file__).resolve().parent
-LIB = pathlib.Path(os.environ.get("ORACLE_LIB_PATH", ORACLE_DIR / "_build" / "liboracle.so"))
+
+
+def _host_has_fma() -> bool:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("flags"):
+                return " fma " in f" {line.split(':', 1)[1].strip()} "
+    except OSError:
+        pass
+    return False
+
+
+# liboracle.so is built with -mfma (hardware fmaf, the same bits as libm's); a CPU without FMA loads
+# the generic build of the same source
+LIB = pathlib.Path(os.environ.get("ORACLE_LIB_PATH", ORACLE_DIR / "_build" / (
+    "liboracle.so" if _host_has_fma() else "liboracle_generic.so")))
+# contract variants of the tolerance measurement (srt_oracle.c ORACLE_CONTRACT): "A" is the kernel's
+CONTRACTS = ("A", "B", "C", "D", "E")
 
 P = C.c_void_p
 
@@ -42,19 +59,20 @@ class OrStats(C.Structure):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
 
 
-_lib = None
+_libs: dict = {}
 
 
 def build():
     subprocess.run(["make", "-s", "-C", str(ORACLE_DIR)], check=True)
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not LIB.exists():
+def lib(contract: str = "A"):
+    """The oracle library of contract variant `contract` (A: the kernel's contract)."""
+    if contract not in _libs:
+        path = LIB if contract == "A" else ORACLE_DIR / "_build" / f"liboracle_{contract}.so"
+        if not path.exists():
             build()
-        L = C.CDLL(str(LIB))
+        L = C.CDLL(str(path))
         L.oracle_dispatch.argtypes = [C.POINTER(OrScene), C.POINTER(OrFrame), P, P, C.c_int, C.c_int,
                                       C.POINTER(OrStats)]
         L.oracle_render.argtypes = [C.POINTER(OrScene), C.POINTER(OrFrame), C.c_int, C.c_int, P, P, C.c_int,
@@ -71,8 +89,11 @@ def lib():
         L.oracle_pow5.restype = C.c_float
         L.oracle_rand_float.argtypes = [C.c_float, C.c_float]
         L.oracle_rand_float.restype = C.c_float
-        _lib = L
-    return _lib
+        L.oracle_contract.restype = C.c_int
+        if chr(L.oracle_contract()) != contract:
+            raise RuntimeError(f"{path}: built for contract {chr(L.oracle_contract())}, not {contract}")
+        _libs[contract] = L
+    return _libs[contract]
 
 
 def _p(a):
@@ -82,7 +103,8 @@ def _p(a):
 class Oracle:
     """Holds the reference-layout inputs of one scene + noise + lights."""
 
-    def __init__(self, scene=None, lights=None, noise=None, noise_u=None):
+    def __init__(self, scene=None, lights=None, noise=None, noise_u=None, contract: str = "A"):
+        self._lib = lib(contract)
         self._keep = []
         s = OrScene()
         if scene is not None:
@@ -133,14 +155,14 @@ class Oracle:
 
     def dispatch(self, f: OrFrame, accum: np.ndarray, out: np.ndarray, y0=0, y1=None) -> dict:
         st = OrStats()
-        lib().oracle_dispatch(C.byref(self.scene), C.byref(f), _p(accum), _p(out), y0,
+        self._lib.oracle_dispatch(C.byref(self.scene), C.byref(f), _p(accum), _p(out), y0,
                               f.height if y1 is None else y1, C.byref(st))
         return st.as_dict()
 
     def render(self, f: OrFrame, frame_first: int, nframes: int, accum: np.ndarray, out: np.ndarray, y0=0, y1=None,
                threads=0) -> dict:
         st = OrStats()
-        lib().oracle_render(C.byref(self.scene), C.byref(f), frame_first, nframes, _p(accum), _p(out), y0,
+        self._lib.oracle_render(C.byref(self.scene), C.byref(f), frame_first, nframes, _p(accum), _p(out), y0,
                             f.height if y1 is None else y1, threads, C.byref(st))
         return st.as_dict()
 
@@ -148,7 +170,7 @@ class Oracle:
                     threads=0) -> dict:
         rows = np.ascontiguousarray(rows, np.int32)
         st = OrStats()
-        lib().oracle_render_rows(C.byref(self.scene), C.byref(f), frame_first, nframes, _p(accum), _p(out), _p(rows),
+        self._lib.oracle_render_rows(C.byref(self.scene), C.byref(f), frame_first, nframes, _p(accum), _p(out), _p(rows),
                                  len(rows), threads, C.byref(st))
         return st.as_dict()
 
@@ -159,7 +181,7 @@ class Oracle:
         t = np.zeros(n, np.float32)
         nrm = np.zeros((n, 3), np.float32)
         st = OrStats()
-        lib().oracle_trace_closest(C.byref(self.scene), bvh_count, _p(rays), n, _p(hits), _p(t), _p(nrm),
+        self._lib.oracle_trace_closest(C.byref(self.scene), bvh_count, _p(rays), n, _p(hits), _p(t), _p(nrm),
                                    C.byref(st))
         return hits, t, nrm, st.as_dict()
 

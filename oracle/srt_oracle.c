@@ -4,10 +4,26 @@
  * Scalar C restatement of the reference GLSL path tracer.  Every function
  * cites the reference file:line it follows.  Arithmetic contract (DESIGN.md
  * section 3): IEEE fp32, source-order evaluation, no FMA contraction
- * (-ffp-contract=off), correctly rounded '/' and sqrt, GLSL min/max/clamp with
- * IEEE minNum/maxNum NaN handling, sin/cos/pow by the double-precision
- * procedures below (shared specification with the HIP kernel, written out
- * independently here).
+ * (-ffp-contract=off) outside the dot/cross built-ins, correctly rounded '/'
+ * and sqrt, GLSL min/max/clamp with IEEE minNum/maxNum NaN handling, sin/cos/pow
+ * by the procedures below (shared specification with the HIP kernel, written
+ * out independently here).
+ *
+ * ORACLE_CONTRACT selects a contract variant (oracle/Makefile builds one
+ * library per variant).  Only the tolerance measurement uses the variants
+ * (tools/contract_tolerance.py, tests/test_contract_tolerance.py): GLSL leaves
+ * these choices to the implementation, so how far the converged image moves
+ * between them bounds what "matches the GLSL render" can mean.
+ *   0 (A) the kernel's contract (the default library, liboracle.so);
+ *   1 (B) no FMA anywhere in expressions: dot/cross/luminance and the RNG
+ *         seed's dot unfused (SURVEY.md 8a's original contract);
+ *   2 (C) every a*b+c contracted, as a fusing GLSL compiler does: A compiled
+ *         with -ffp-contract=fast -mfma (GetRay's pixelSample, the hit point
+ *         dist*dir+origin, SampleDiffuse's sums, the BRDF terms, ...);
+ *   3 (D) sin/cos in double precision rounded to float (correctly rounded
+ *         unless the double result lies within 2^-29 ulp of a float midpoint);
+ *   4 (E) B and D together: the round-1 contract (tests/golden/
+ *         contract_e_renders.json pins it against that round's golden renders).
  */
 #include "srt_oracle.h"
 
@@ -32,12 +48,25 @@ static inline v3 muls(v3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
 static inline v3 smul(float s, v3 a) { return V(s * a.x, s * a.y, s * a.z); }
 static inline v3 divs(v3 a, float s) { return V(a.x / s, a.y / s, a.z / s); }
 static inline v3 neg(v3 a) { return V(-a.x, -a.y, -a.z); }
+#ifndef ORACLE_CONTRACT
+#define ORACLE_CONTRACT 0
+#endif
+#define CTR_UNFUSED (ORACLE_CONTRACT == 1 || ORACLE_CONTRACT == 4)  /* B, E */
+#define CTR_DSIN (ORACLE_CONTRACT == 3 || ORACLE_CONTRACT == 4)     /* D, E */
+#if CTR_UNFUSED
+/* variants B, E: the built-ins as written, left to right, every product rounded */
+static inline float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline v3 cross(v3 a, v3 b) {
+  return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+#else
 /* GLSL dot / cross built-ins with fused multiply-adds:
  * dot = fma(z, z', fma(y, y', x * x')), cross_i = fma(a_j, b_k, -(a_k * b_j)). */
 static inline float dot(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 static inline v3 cross(v3 a, v3 b) {
   return V(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
 }
+#endif
 static inline float length3(v3 a) { return sqrtf(dot(a, a)); }
 static inline v3 normalize3(v3 a) { float inv = 1.0f / sqrtf(dot(a, a)); return muls(a, inv); }
 /* GLSL min/max with IEEE minNum/maxNum NaN handling (the non-NaN operand wins). */
@@ -61,6 +90,28 @@ static inline v3 vload(const float* p) { return V(p[0], p[1], p[2]); }
  * sinf/cosf minimax polynomials on [-pi/4, pi/4] and the quadrant's
  * sign/selection.  |x| >= 2^30 gives 0, NaN and Inf give NaN.  The kernel
  * (simple-ray-tracer_amd/csrc/pt_math.hpp) evaluates the same expressions. */
+#if CTR_DSIN
+/* variants D, E: double-precision Cody-Waite reduction (pi/2 in two parts) and
+ * the fdlibm kernel polynomials, rounded once to float (the round-1 contract) */
+static void sincos_kernel(float xf, int want_cos, float* out) {
+  if (xf != xf || xf == INFINITY || xf == -INFINITY) { *out = NAN; return; }
+  if (fabsf(xf) >= 0x1p30f) { *out = 0.0f; return; }
+  const double x = (double)xf;
+  const double kd = rint(x * 0x1.45f306dc9c883p-1);
+  const long long k = (long long)kd;
+  const double r = (x - kd * 0x1.921fb54400000p+0) - kd * 0x1.0b4611a626331p-34;
+  const double z = r * r;
+  const double s = r + (r * z) * (-1.66666666666666324348e-01 + z * (8.33333333332248946124e-03 +
+                   z * (-1.98412698298579493134e-04 + z * (2.75573137070700676789e-06 +
+                   z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)))));
+  const double c = (1.0 - 0.5 * z) + (z * z) * (4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 +
+                   z * (2.48015872894767294178e-05 + z * (-2.75573143513906633035e-07 +
+                   z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+  const int q = (int)((k + (want_cos ? 1 : 0)) & 3);
+  const double v = (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
+  *out = (float)v;
+}
+#else
 static void sincos_kernel(float x, int want_cos, float* out) {
   if (x != x || x == INFINITY || x == -INFINITY) { *out = NAN; return; }
   if (fabsf(x) >= 0x1p30f) { *out = 0.0f; return; }
@@ -77,6 +128,7 @@ static void sincos_kernel(float x, int want_cos, float* out) {
   const float v = (q & 1) ? c : s;
   *out = (q & 2) ? -v : v;
 }
+#endif
 float oracle_sin(float x) { float r; sincos_kernel(x, 0, &r); return r; }
 float oracle_cos(float x) { float r; sincos_kernel(x, 1, &r); return r; }
 
@@ -148,6 +200,9 @@ float oracle_pow(float x, float y) {
  * rounded to nearest-even for every x whose result is a normal float (checked
  * over all 2^32 inputs against the exact value: tools/pow5_exhaustive.hip).
  * GLSL domain as oracle_pow: x < 0 and NaN -> NaN, +-0 -> +0. */
+/* variant tag of this build: 'A' + ORACLE_CONTRACT */
+int oracle_contract(void) { return 'A' + ORACLE_CONTRACT; }
+
 float oracle_pow5(float x) {
   if (!(x >= 0.0f)) return NAN;
   if (x == 0.0f) return 0.0f;
@@ -194,7 +249,11 @@ typedef struct {
 
 /* raytrace_utils.glsl:28-30 */
 float oracle_rand_float(float sx, float sy) {
+#if CTR_UNFUSED
+  float d = sx * 12.9898f + sy * 78.233f;
+#else
   float d = fmaf(sy, 78.233f, sx * 12.9898f);  /* dot(seed, vec2(12.9898, 78.233)) */
+#endif
   float m = oracle_sin(d) * 43758.5453f;
   return fractf(m);
 }

@@ -112,6 +112,8 @@ float oracle_cos(float x);
 float oracle_pow(float x, float y);
 float oracle_pow5(float x);
 float oracle_rand_float(float sx, float sy);
+/* 'A' + ORACLE_CONTRACT of this build (srt_oracle.c: the contract variants) */
+int oracle_contract(void);
 
 #ifdef __cplusplus
 }

@@ -47,6 +47,7 @@ struct KParams {
   float4* lbuf;            // sample buffer: nframes x local_pixels radiance samples
   int local_pixels;        // W * local_rows
   int trav_frac16;         // resume shading when fewer than trav_frac16/16 of working lanes traverse
+  int bounce_cap;          // bounces after which a path is cut (and counted in ST_BOUNCECAP)
   int stack_base_f4;       // first float4 of the per-lane stacks in dynamic LDS
   uint32_t* gstack;        // global-scene mode: per-lane stacks in HBM, entry field k of lane g at gstack[k * stride + g]
   int gstack_stride;       // lanes in the grid
@@ -68,6 +69,7 @@ struct KParams {
 extern __shared__ __attribute__((aligned(16))) float4 g_smem[];
 
 enum { ST_RAYS = 0, ST_NODES, ST_TRIS, ST_RNGU, ST_RNGSQ, ST_LIGHTS, ST_MATS, ST_SAMPLES, ST_OVERFLOW, ST_MAXSTACK,
+       ST_BOUNCECAP,  // paths cut at the bounce cap (KParams::bounce_cap)
        ST_N, ST_CYC_REFILL = ST_N, ST_CYC_TRAV, ST_CYC_SHADE, ST_CYC_ITERS,
        // lane occupancy of the traversal loop (summed popcounts per iteration) and of shading
        ST_DBG_TITERS, ST_DBG_WORK, ST_DBG_TRAV, ST_DBG_LEAF, ST_DBG_INT, ST_DBG_SHADE,

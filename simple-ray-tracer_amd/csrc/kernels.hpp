@@ -34,9 +34,6 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
 #ifndef SRT_TILE_SCHED
 #define SRT_TILE_SCHED 1  // tiles of each frame in the last launch's cost order
 #endif
-#ifndef SRT_BOUNCE_CAP
-#define SRT_BOUNCE_CAP (1 << 20)  // bounces after which a path is cut (and counted in stack_overflow)
-#endif
 
 #ifndef SRT_GLOBAL_WAVES
 #define SRT_GLOBAL_WAVES 4
@@ -455,11 +452,12 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
         }
 
         // The reference's loop has no depth cap (Russian roulette clamps the
-        // survival probability to >= 0.1).  A path still alive after 2^20
-        // bounces is cut (and counted) so a pathological scene cannot hang the GPU.
-        if (++bounces >= SRT_BOUNCE_CAP && !term) {
+        // survival probability to >= 0.1).  A path still alive after
+        // kp.bounce_cap bounces (2^20 unless SRT_BOUNCE_CAP says otherwise) is
+        // cut and counted, so a pathological scene cannot hang the GPU.
+        if (++bounces >= kp.bounce_cap && !term) {
           term = true;
-          bump<COUNT>(c, ST_OVERFLOW);
+          bump<COUNT>(c, ST_BOUNCECAP);
         }
         ro = p;
         if (selected) {  // trace CheckLightOccluded's ray next (t in (0.001, |light - p|))
@@ -588,15 +586,18 @@ __global__ __launch_bounds__(256) void reset_kernel(KParams kp) {
 }
 
 // The closest-hit test kernel of ray_intersects.glsl:135-161.
-// Stacks in LDS (stride = block), or lane-interleaved in HBM when `gstk` is given (deep trees).
+// Stacks in LDS (stride = block), or in HBM when `gstk` is given (deep trees): each block
+// has its own area of blockDim.x * 3 * stack_entries dwords, lane-interleaved within it, so
+// the in-area index stays far below 2^31 for any ray count (the area's base is 64-bit).
 __global__ __launch_bounds__(256) void closest_kernel(KParams kp, const srt_ray* rays, uint32_t n, uint32_t* hits,
                                                       float* tout, uint32_t* gstk) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Lane ln;
   ln.base = 0;
-  ln.stk = gstk ? gstk + i : reinterpret_cast<uint32_t*>(g_smem) + threadIdx.x;
-  ln.stride = gstk ? (int)n : (int)blockDim.x;
+  ln.stk = gstk ? gstk + (size_t)blockIdx.x * blockDim.x * 3u * (uint32_t)kp.stack_entries + threadIdx.x
+                : reinterpret_cast<uint32_t*>(g_smem) + threadIdx.x;
+  ln.stride = (int)blockDim.x;
   Counters c;
   for (int k = 0; k < ST_N; ++k) c.v[k] = 0;
   const srt_ray r = rays[i];

@@ -129,6 +129,7 @@ struct srt_context {
   size_t lbuf_cap = (size_t)16 << 30;  // SRT_SAMPLE_BUFFER_MB
   int tail_claims = 16;  // SRT_TAIL_CLAIMS: claims per wave before the end from which claims take one batch
   int trav_frac16 = 9;                 // SRT_TRAV_FRAC16 (measured best on Rubik 1080p with the 16-sub-step pattern)
+  int bounce_cap = 1 << 20;            // SRT_BOUNCE_CAP: bounces after which a path is cut (counted)
   int trav_frac16_global = 9;          // SRT_TRAV_FRAC16_GLOBAL: the same threshold for global-scene mode
   int num_cus = 256;
   // stats
@@ -446,6 +447,7 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   }
   kp.lbuf = c->d_lbuf;
   kp.trav_frac16 = ldsm ? c->trav_frac16 : c->trav_frac16_global;
+  kp.bounce_cap = c->bounce_cap;
   HIP_OK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_TOTAL, c->stream));
   const int out_frames = kp.frame_first + kp.nframes - 1;
   const int nchunks = (kp.nframes + chunk - 1) / chunk;
@@ -516,6 +518,7 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
     c->stats.mat_reads += s[srt::ST_MATS];
     c->stats.samples += s[srt::ST_SAMPLES];
     c->stats.stack_overflow += s[srt::ST_OVERFLOW];
+    c->stats.bounce_cap += s[srt::ST_BOUNCECAP];
     c->stats.max_stack = std::max<uint64_t>(c->stats.max_stack, s[srt::ST_MAXSTACK]);
   }
   return SRT_OK;
@@ -575,8 +578,9 @@ int ValidateNodes(const srt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_tris, 
 // 0 keeps node 0 (the ghost zero records traverse from it); other roots take a
 // pair's first slot with a zero record beside it.  Returns false (the identity
 // layout is used) for inputs whose sibling pairs overlap, which no
-// reference-built tree has; the kernel checks adjacency itself, so any layout
-// stays exact.
+// reference-built tree has.  A child pair reached from two BVH records' trees
+// keeps its first placement; srt_upload_scene sets a node's "right child's
+// pair follows" flag only where the remapped slots confirm it.
 bool LayoutNodes(const srt_bvh_node* nodes, uint32_t n_nodes, const srt_bvh_record* bvhs, uint32_t n_bvhs,
                  bool align, std::vector<uint32_t>* remap, uint32_t* n_slots) {
   constexpr uint32_t kUnset = 0xFFFFFFFFu;
@@ -641,6 +645,7 @@ int srt_create(int device, void* stream, srt_context** out) {
   if (const char* e = std::getenv("SRT_FORCE_GLOBAL_SCENE")) c->force_global = e[0] == '1';
   if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_MB")) c->lbuf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
   if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_KB")) c->lbuf_cap = (size_t)std::max(1L, std::atol(e)) << 10;
+  if (const char* e = std::getenv("SRT_BOUNCE_CAP")) c->bounce_cap = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("SRT_TAIL_CLAIMS")) c->tail_claims = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("SRT_TILE_ORDER")) c->tile_schedule = e[0] != '0';
   if (const char* e = std::getenv("SRT_TRAV_FRAC16")) c->trav_frac16 = std::max(0, std::min(16, std::atoi(e)));
@@ -909,8 +914,14 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
     const srt_bvh_node& n = nodes[i];
     uint32_t first = n.first_child_or_prim_index;
     if (n.prim_count == 0) {  // internal: c0's slot, less 1 when c1 is internal (its pair then follows)
+      // The flag promises that c1's own child pair is the next pair of the array.  LayoutNodes
+      // places it there whenever it lays the pair out itself; a pair shared with an earlier
+      // BVH record's tree keeps its first placement, so the flag is set only when the
+      // remapped slots say so.
+      const uint32_t c0 = n.first_child_or_prim_index;
+      const srt_bvh_node& n1 = nodes[c0 + 1];
       first = remap[first];
-      if (laid && nodes[n.first_child_or_prim_index + 1].prim_count == 0) first -= 1;
+      if (laid && n1.prim_count == 0 && remap[n1.first_child_or_prim_index] == remap[c0] + 2) first -= 1;
       if (((first | (laid ? 1u : 0u)) & 1u) == 0) pairs_aligned = false;  // overlapping sibling pairs
     }
     float w0, w1;
@@ -1288,10 +1299,11 @@ int srt_trace_closest(srt_context* c, const srt_ray* rays, uint32_t n, uint32_t*
   HIP_OK(hipMalloc(&d_rays.p, sizeof(srt_ray) * n));
   HIP_OK(hipMalloc(&d_hits.p, sizeof(uint32_t) * n));
   HIP_OK(hipMalloc(&d_t.p, sizeof(float) * n));
-  if (hbm_stack) HIP_OK(hipMalloc(&d_stk.p, entry * n));
+  const size_t grid = (n + block - 1) / block;
+  if (hbm_stack) HIP_OK(hipMalloc(&d_stk.p, entry * grid * (size_t)block));  // one area per block
   HIP_OK(hipMemcpyAsync(d_rays.p, rays, sizeof(srt_ray) * n, hipMemcpyHostToDevice, c->stream));
   HIP_OK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_N, c->stream));
-  hipLaunchKernelGGL(srt::closest_kernel, dim3((n + block - 1) / block), dim3(block), lds, c->stream, kp,
+  hipLaunchKernelGGL(srt::closest_kernel, dim3((unsigned)grid), dim3(block), lds, c->stream, kp,
                      static_cast<const srt_ray*>(d_rays.p), n, static_cast<uint32_t*>(d_hits.p),
                      static_cast<float*>(d_t.p), static_cast<uint32_t*>(d_stk.p));
   HIP_OK(hipGetLastError());

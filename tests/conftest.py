@@ -52,12 +52,13 @@ def bits_equal(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     return same | (np.isnan(a) & np.isnan(b))
 
 
-def oracle_render(setup, spp: int, rows=None, threads: int = 0):
-    """Reset frame + `spp` progressive frames on the CPU oracle (full frame or given rows)."""
+def oracle_render(setup, spp: int, rows=None, threads: int = 0, contract: str = "A"):
+    """Reset frame + `spp` progressive frames on the CPU oracle (full frame or given rows), in the
+    kernel's arithmetic contract or one of the variants (oracle/srt_oracle.c ORACLE_CONTRACT)."""
     from oracle import pyoracle as O
 
     s = setup
-    orc = O.Oracle(s.scene, s.lights, s.noise, s.noise_u)
+    orc = O.Oracle(s.scene, s.lights, s.noise, s.noise_u, contract=contract)
     cam = s.camera
     f = O.Oracle.frame(s.width, s.height, show_model=s.show_model, bvh_count=s.bvh_count, light_count=len(s.lights),
                        max_depth=s.max_depth, origin=cam.position, direction=cam.front, up=cam.up, right=cam.right)

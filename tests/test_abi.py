@@ -34,7 +34,7 @@ def test_python_binding_covers_header():
 
     assert set(declared_functions()) == set(_lib.EXPORTED_SYMBOLS)
     lib = _lib.lib()
-    assert lib.srt_abi_version() == 1
+    assert lib.srt_abi_version() == 2
     for n in declared_functions():
         assert isinstance(getattr(lib, n), ctypes._CFuncPtr)
 

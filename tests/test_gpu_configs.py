@@ -230,3 +230,38 @@ def test_deep_tree_closest_hit_and_render():
     gacc, gout, gst = gpu_render(setup, 2)
     assert bits_equal(gacc, acc).all() and (gout == out).all()
     assert gst["rays"] == st["rays"] and gst["stack_overflow"] == 0
+
+
+def test_deep_tree_hbm_stacks_past_2g_entries():
+    """The closest-hit kernel's HBM stacks (trees too deep for LDS stacks) with more rays than a flat
+    lane-interleaved layout could index in 32 bits: 9 M rays x 3 dwords x ~100 entries is past 2^31
+    (ADVICE r02).  The 400 distinct rays of test_deep_tree_closest_hit_and_render are repeated; every
+    copy must return the oracle's hit and distance."""
+    from oracle import pyoracle as O
+
+    model = S.model_from_triangles(_deep_chain(), kd=(0.6, 0.6, 0.6), ks=(0.1, 0.1, 0.1), ns=8.0)
+    scene = S.Scene.from_models([model])
+    depth = model.info()["max_depth"]
+    n = 200
+    base = np.zeros(2 * n, S.RAY_DTYPE)
+    x = np.float32(1.5) ** np.arange(n).astype(np.float32)
+    base["o"][:n, 0] = x
+    base["o"][:n, 2] = np.float32(10.0) * x
+    base["d"][:n] = (0.0, 0.0, -1.0)
+    base["o"][n:] = (-2.0, 0.01, 0.0)
+    base["d"][n:, 0] = 1.0
+    base["d"][n:, 1] = np.linspace(-0.2, 0.2, n, dtype=np.float32)
+    base["t"] = np.float32(1e30)
+    hits_o, t_o, _, _ = O.Oracle(scene).trace_closest(1, base)
+    reps = 22500  # 9,000,000 rays
+    assert reps * len(base) * 3 * (depth + 1) > 2 ** 31
+    rays = np.tile(base, reps)
+    c = S.Compute().Init()
+    try:
+        c.bind_scene(scene)
+        c.SetUInt("bvh_count", 1)
+        hits, t = c.trace_closest(rays)
+    finally:
+        c.close()
+    assert (hits.reshape(reps, -1) == hits_o).all()
+    assert bits_equal(t.reshape(reps, -1), np.broadcast_to(t_o, (reps, len(base)))).all()

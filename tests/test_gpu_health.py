@@ -74,6 +74,35 @@ def test_nan_samples_counted(rubik):
         r.close()
 
 
+def test_bounce_cap_counted_apart_from_stack_overflow(rubik, monkeypatch):
+    """Paths cut at the bounce cap have their own counter (srt_stats.bounce_cap), so an embedder can tell
+    them from traversal stack overflows.  The reference's loop has no cap; the default (2^20) cuts nothing
+    here and the frame is the oracle's, while SRT_BOUNCE_CAP=2 cuts every path still alive after two
+    bounces and counts them, with no stack overflow."""
+    setup = R.make_setup(40, 32, show_model=True, models=[rubik], max_depth=8)
+    want_acc, _, want_st = oracle_render(setup, 2)
+    r = R.Renderer(setup)
+    try:
+        r.render(2, count=True)
+        r.finish()
+        st = r.compute.stats()
+        assert bits_equal(r.accum(), want_acc).all()
+        assert st["bounce_cap"] == 0 and st["stack_overflow"] == 0
+    finally:
+        r.close()
+    monkeypatch.setenv("SRT_BOUNCE_CAP", "2")
+    r = R.Renderer(setup)
+    try:
+        r.render(2, count=True)
+        r.finish()
+        st = r.compute.stats()
+        assert st["bounce_cap"] > 0 and st["stack_overflow"] == 0
+        assert st["rays"] < want_st["rays"]
+        assert not bits_equal(r.accum(), want_acc).all()
+    finally:
+        r.close()
+
+
 def test_checkpoint_resume_is_bit_identical(rubik, tmp_path):
     setup = R.make_setup(48, 40, show_model=True, models=[rubik])
     want_acc, want_out, _ = oracle_render(setup, 5)

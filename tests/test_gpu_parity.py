@@ -217,6 +217,35 @@ def test_node_layouts_global_mode(monkeypatch, env):
     assert_parity(two, 2)
 
 
+@pytest.mark.parametrize("force_global", ["1", "0"])
+def test_bvh_records_sharing_a_subtree(rubik, monkeypatch, force_global):
+    """Two BVH records whose trees share subtrees: the second record's root is a new node
+    whose child pair copies the first tree's root children, child indices included, so both trees reach
+    the same grandchild pairs.  The device layout places a shared pair once, under the first tree; the
+    second tree's new pair is laid elsewhere, so its node must not claim that its right child's pair
+    follows it (the global-mode right-spine step would read the wrong pair).  The second record is
+    moved so both trees are hit."""
+    import dataclasses
+
+    monkeypatch.setenv("SRT_FORCE_GLOBAL_SCENE", force_global)
+    setup = R.make_setup(48, 40, show_model=True, models=[rubik])
+    n = setup.scene.nodes
+    L = len(n)
+    c0 = int(n[0]["first"])
+    assert n[0]["count"] == 0 and n[c0 + 1]["count"] == 0  # the root's right child is internal
+    m = np.concatenate([n, np.zeros(3, n.dtype)])
+    m[L] = n[0]
+    m[L]["first"] = L + 1
+    m[L + 1], m[L + 2] = n[c0], n[c0 + 1]  # copies: their children are the first tree's pairs
+    bvhs = np.concatenate([setup.scene.bvhs, setup.scene.bvhs[:1]])
+    bvhs[1]["first_index"] = L
+    frame = np.eye(4, dtype=np.float32)
+    frame[3, :3] = (7.0, -1.0, -3.0)
+    bvhs[1]["frame"] = frame.reshape(16)
+    shared = dataclasses.replace(setup, scene=dataclasses.replace(setup.scene, nodes=m, bvhs=bvhs), bvh_count=2)
+    assert_parity(shared, 2)
+
+
 @pytest.mark.parametrize("layout", ["1", "0"])
 def test_lds_mode_node_orders(rubik, monkeypatch, layout):
     """LDS mode reads node pairs from 80-B blocks (traversal.hpp node_pair) in both device orders: the
