@@ -123,16 +123,32 @@ def load_counters(workload: str):
         return None
 
 
+def code_hash() -> str:
+    """srt_code_hash() of the loaded library: its kernel sources + hipcc flags."""
+    from srt_amd import _lib
+
+    return _lib.lib().srt_code_hash().decode()
+
+
 def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str, global_mode: bool = False) -> dict:
     """Roofs of the dominant kernel, fractions of the live kernel time (HIP events on the launch stream):
     VALU issue (SQ_INSTS_VALU x 2 cycles per SIMD-32 over 1024 SIMDs), LDS-array cycles
     (SQ_LDS_IDX_ACTIVE over 256 CUs), HBM (corrected FETCH_SIZE + WRITE_SIZE over 8 TB/s).  The counters
-    are per launch of this workload, from profiles/counters.json; `bound` is the highest fraction."""
+    are per launch of this workload, from profiles/counters.json, and count only when they were collected
+    on the code that is timed (their code_hash equals the loaded library's); `bound` is the highest
+    fraction."""
     k_s = k_ms * 1e-3
     alg_gbs = alg_bytes / k_s / 1e9
+    here = code_hash()
     r = {"kernel": kernel_name, "kernel_ms": round(k_ms, 3), "algorithmic_bytes_per_launch": int(alg_bytes),
-         "algorithmic_GBps": round(alg_gbs, 1)}
+         "algorithmic_GBps": round(alg_gbs, 1), "code_hash": here}
     cnt = load_counters(workload)
+    if cnt is not None and cnt.get("code_hash") != here:
+        r.update({"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
+                  "counters_source": cnt.get("source", ""), "counters_code_hash": cnt.get("code_hash"),
+                  "note": "the committed PMC counters of this workload were collected on other code (their "
+                          "code_hash differs from the loaded library's): roofs not reported until re-captured"})
+        return r
     if cnt is None:
         # no roof can be claimed without counters: algorithmic bytes are mostly LDS / L2 reads, and
         # dividing them by the HBM peak gives fractions above 1 (round-1 VERDICT)
@@ -160,6 +176,7 @@ def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str, globa
         "useful_valu_frac": round(fr["valu_issue"] * cnt["SQ_THREAD_CYCLES_VALU"] / (64.0 * cnt["SQ_INSTS_VALU"]), 4),
         "lds_bank_conflict_frac": round(cnt["SQ_LDS_BANK_CONFLICT"] / max(cnt["SQ_LDS_IDX_ACTIVE"], 1.0), 4),
         "counters_source": cnt.get("source", ""),
+        "counters_code_hash": cnt.get("code_hash"),
         "note": "frac = the bound roof's fraction at the live kernel time; per-launch counters from the committed "
                 "rocprofv3 passes of this workload (profiles/counters.json). The 2.4 GHz peak clock makes every "
                 "fraction a lower bound. " + (
@@ -387,6 +404,7 @@ def main(argv=None):
             "frame_ms": round(ms_per_step / spp, 4),
             "msamples_per_s": round(W * H * spp * args.steps / elapsed_s / 1e6, 3),
             "rays_per_step": int(total_rays),
+            "code_hash": code_hash(),
             # per-rank counters describe rank 0's launch: the roofline is a 1-GPU figure
             "roofline": roofline(wl_name, k_ms, algorithmic_bytes(st), kname, global_mode=args.scene == "synthetic")
             if world == 1 else

@@ -69,6 +69,9 @@ typedef struct srt_scene srt_scene;
 
 const char* srt_last_error(void);
 int srt_abi_version(void);
+/* Identity of this library's device code: a hash of the kernel sources and the hipcc flags they were
+ * built with (16 hex digits).  Measurements keyed to code (profiles/counters.json) carry it. */
+const char* srt_code_hash(void);
 
 /* ===================== Graphics::Compute (the dispatch API) =====================
  * replaces Graphics::Compute(path) + Init() (include/graphics/shader.h:46-55,

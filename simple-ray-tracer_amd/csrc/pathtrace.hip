@@ -636,6 +636,10 @@ extern "C" {
 
 const char* srt_last_error(void) { return srt::LastError(); }
 int srt_abi_version(void) { return SRT_ABI_VERSION; }
+#ifndef SRT_CODE_HASH
+#define SRT_CODE_HASH "unknown"
+#endif
+const char* srt_code_hash(void) { return SRT_CODE_HASH; }
 
 int srt_create(int device, void* stream, srt_context** out) {
   if (!out) return SRT_ERR_INVALID;

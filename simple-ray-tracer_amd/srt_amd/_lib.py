@@ -86,6 +86,7 @@ P = C.c_void_p
 _SIGS = {
     "srt_last_error": (C.c_char_p, []),
     "srt_abi_version": (C.c_int, []),
+    "srt_code_hash": (C.c_char_p, []),
     "srt_create": (C.c_int, [C.c_int, P, C.POINTER(P)]),
     "srt_program_create": (C.c_uint32, [C.c_char_p]),
     "srt_program_delete": (C.c_int, [C.c_uint32]),

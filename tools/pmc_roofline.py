@@ -68,7 +68,22 @@ def per_launch(sub):
     return out
 
 
+def bench_code_hash(sub):
+    """code_hash of the library the pass profiled: bench.py's JSON line in the pass's log (<sub>.log)."""
+    hashes = set()
+    for line in (out_dir / f"{sub}.log").read_text().splitlines():
+        if line.startswith("{"):
+            d = json.loads(line)
+            hashes |= {d["roofline"].get("code_hash")} | {l["roofline"].get("code_hash") for l in d.get("legs", [])}
+    hashes.discard(None)
+    assert len(hashes) == 1, f"{sub}.log: code hashes {hashes}"
+    return hashes.pop()
+
+
 sq, fetch, write = per_launch("pmc_sq"), per_launch("pmc_fetch"), per_launch("pmc_write")
+code = {bench_code_hash(s) for s in ("pmc_sq", "pmc_fetch", "pmc_write")}
+assert len(code) == 1, f"the passes profiled different code: {code}"
+code = code.pop()
 p = root / "profiles" / "counters.json"
 data = json.loads(p.read_text()) if p.exists() else {}
 for wl in sq:
@@ -81,6 +96,7 @@ for wl in sq:
         d.update({k: v for k, v in tcc.items()})
     d["source"] = (f"rocprofv3 --pmc passes ({tag}): SQ counters + GRBM_GUI_ACTIVE, FETCH_SIZE, WRITE_SIZE; "
                    f"python bench.py --steps 1 --warmup 0 --no-cpu-baseline; per launch of the timed step")
+    d["code_hash"] = code
     data[wl] = d
     lane = d["SQ_THREAD_CYCLES_VALU"] / (64 * d["SQ_INSTS_VALU"])
     print(f"{wl}: VALU {d['SQ_INSTS_VALU']:.4g} insts, lane util {lane:.3f}, LDS active {d['SQ_LDS_IDX_ACTIVE']:.4g}, "
