@@ -47,6 +47,21 @@ VALU_PEAK_GIPS = SIMDS * CLOCK_HZ / VALU_ISSUE_CYCLES / 1e9  # 1228.8 G wave-ins
 LDS_PEAK_GCPS = CUS * CLOCK_HZ / 1e9  # 614.4 G LDS-array cycles/s (one per CU per clock)
 
 
+def l2_miss_peak_gbs() -> float:
+    """The memory-side roof for the traversal's reads, measured (tools/gather_calib.hip,
+    profiles/r03_gather_calibration.json): every L2 miss is one 128-B line request (FETCH_SIZE tallies
+    it at 64 B), and random whole-record reads of a table the Infinity Cache holds move at most ~7.2 TB/s
+    of lines; past the Infinity Cache, random lines move at 1.8-5.8 TB/s and a stream at 5.9 TB/s.  The
+    counters cannot tell Infinity-Cache hits from HBM reads, so this roof is 'l2_miss', not 'hbm'."""
+    p = ROOT / "profiles" / "r03_gather_calibration.json"
+    try:
+        cases = json.loads(p.read_text())["cases"]
+        return max(c["dram_32B_bytes"] / (c["ms"] * 1e-3) / 1e9 for c in cases
+                   if c["case"] != "stream" and c["table_MiB"] < 256)
+    except Exception:
+        return HBM_PEAK_GBS
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -163,7 +178,7 @@ def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str, globa
     roofs = {
         "valu_issue": (valu_gips, VALU_PEAK_GIPS, "G VALU wave-instructions/s"),
         "lds": (lds_gcps, LDS_PEAK_GCPS, "G LDS-array cycles/s"),
-        "hbm": (hbm_gbs, HBM_PEAK_GBS, "GB/s"),
+        "l2_miss": (hbm_gbs, l2_miss_peak_gbs(), "GB/s of L2-miss lines (Infinity Cache or HBM)"),
     }
     fr = {k: a / p for k, (a, p, _) in roofs.items()}
     bound = max(fr, key=fr.get)
@@ -171,6 +186,7 @@ def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str, globa
     r.update({
         "bound": bound, "achieved": round(a, 2), "peak": p, "unit": u, "frac": round(a / p, 4),
         "traffic": int(hbm_bytes),
+        "traffic_over_hbm_spec": round(hbm_gbs / HBM_PEAK_GBS, 4),
         "fractions": {k: round(v, 4) for k, v in fr.items()},
         "valu_lane_utilisation": round(cnt["SQ_THREAD_CYCLES_VALU"] / (64.0 * cnt["SQ_INSTS_VALU"]), 4),
         "useful_valu_frac": round(fr["valu_issue"] * cnt["SQ_THREAD_CYCLES_VALU"] / (64.0 * cnt["SQ_INSTS_VALU"]), 4),
@@ -180,7 +196,9 @@ def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str, globa
         "note": "frac = the bound roof's fraction at the live kernel time; per-launch counters from the committed "
                 "rocprofv3 passes of this workload (profiles/counters.json). The 2.4 GHz peak clock makes every "
                 "fraction a lower bound. " + (
-                    "hbm = the L2 misses' bytes (2 x FETCH_SIZE + WRITE_SIZE), served by the Infinity Cache or HBM; "
+                    "l2_miss = the L2 misses' 128-B lines (2 x FETCH_SIZE + WRITE_SIZE, calibrated: "
+                    "profiles/r03_gather_calibration.json), served by the Infinity Cache or HBM, over the measured "
+                    "line-rate roof; traffic = those bytes per launch; "
                     "algorithmic_GBps = SURVEY 8d bytes per launch / kernel time (L2 hits included)." if global_mode
                     else "algorithmic_GBps = SURVEY 8d bytes per launch / kernel time: the scene is read from LDS "
                          "and the noise from L2, so it is not an HBM rate."),

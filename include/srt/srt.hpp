@@ -8,6 +8,7 @@
 //   AssetUtils::UploadModelDataToGPU / UpdateModelMatrix / UpdateRays
 //                                src/asset_utils/gpu_loader.cpp:63-210
 //   RayTracer::Camera / PointLight   src/raytracer/camera.cpp, include/raytracer/light.h
+//   Graphics::ComputeGroup       (new) the same loop's frame tiled over several GPUs (srt_group_*)
 // GL's "currently bound program" is mirrored by Compute::Use(): the upload
 // functions act on the last used Compute, as they act on the bound GL state.
 // Errors: std::runtime_error (the reference std::terminate()s in Init and
@@ -169,6 +170,93 @@ class Compute {
   bool images_dirty_ = true;
   int img_w_ = -1, img_h_ = -1;
   int width_ = 0;
+};
+
+// The frame of main.cpp's loop tiled over several GPUs of this process (srt_group_*): one
+// Compute per device; uniforms and bindings go to every device; Dispatch / RenderFrames render each
+// device's row bands, gather them to the first device over RCCL and assemble the full frame there.
+//   Graphics::ComputeGroup rt("./shaders/raytrace_compute.glsl", {0, 1, 2, 3, 4, 5, 6, 7});
+//   rt.ForEach([&](Graphics::Compute& c) { c.Use(); AssetUtils::UploadModelDataToGPU({model.get()}, 5); });
+//   ... rt.SetInt("accumFrames", accumFrames); rt.Dispatch(W / 8, H / 8); rt.Finish(); ...
+class ComputeGroup {
+ public:
+  ComputeGroup(const char* path, const std::vector<int>& devices, int band_rows = 8) : band_rows_(band_rows) {
+    if (devices.empty()) throw std::runtime_error("ComputeGroup: no devices");
+    for (int d : devices) parts_.push_back(std::make_unique<Compute>(path, d));
+  }
+  ~ComputeGroup() {
+    if (g_) srt_group_destroy(g_);
+  }
+  ComputeGroup(const ComputeGroup&) = delete;
+  ComputeGroup& operator=(const ComputeGroup&) = delete;
+
+  size_t size() const { return parts_.size(); }
+  Compute& operator[](size_t i) { return *parts_[i]; }
+  template <class F>
+  void ForEach(F f) {
+    for (auto& c : parts_) f(*c);
+  }
+  srt_group* group() {
+    if (!g_) {
+      std::vector<srt_context*> ctxs;
+      for (auto& c : parts_) ctxs.push_back(c->context());
+      check(srt_group_create(ctxs.data(), (int)ctxs.size(), band_rows_, &g_), "ComputeGroup");
+    }
+    return g_;
+  }
+  const char* Transport() { return srt_group_transport(group()); }
+
+  void SetBool(const std::string& n, bool v) { ForEach([&](Compute& c) { c.SetBool(n, v); }); }
+  void SetInt(const std::string& n, int v) {
+    ForEach([&](Compute& c) { c.SetInt(n, v); });
+    if (n == "Width" && v != w_) w_ = v, images_dirty_ = true;
+    if (n == "Height" && v != h_) h_ = v, images_dirty_ = true;
+  }
+  void SetUInt(const std::string& n, uint32_t v) { ForEach([&](Compute& c) { c.SetUInt(n, v); }); }
+  void SetVec3(const std::string& n, const vec3& v) { ForEach([&](Compute& c) { c.SetVec3(n, v); }); }
+  void BindNoise(const std::vector<float>& a, const std::vector<float>& b) {
+    ForEach([&](Compute& c) { c.BindNoise(a, b); });
+  }
+  void BindLights(const std::vector<srt_light>& l) { ForEach([&](Compute& c) { c.BindLights(l); }); }
+
+  // glDispatchCompute on every device, the gather and the full frame (src/main.cpp:706)
+  void Dispatch(uint32_t gx, uint32_t gy, uint32_t gz = 1) {
+    if (gz != 1) throw std::runtime_error("Dispatch: groups_z must be 1");
+    Images();
+    check(srt_group_dispatch(group(), gx, gy), "ComputeGroup::Dispatch");
+  }
+  void RenderFrames(int frame_first, int n) {
+    Images();
+    check(srt_group_render_frames(group(), frame_first, n), "ComputeGroup::RenderFrames");
+  }
+  void Finish() { check(srt_group_finish(group()), "ComputeGroup::Finish"); }
+  std::vector<float> ReadAccum() {
+    std::vector<float> v((size_t)w_ * h_ * 4);
+    check(srt_group_read_accum(group(), v.data(), v.size() * sizeof(float)), "ComputeGroup::ReadAccum");
+    return v;
+  }
+  std::vector<uint8_t> ReadOutput() {
+    std::vector<uint8_t> v((size_t)w_ * h_ * 4);
+    check(srt_group_read_output(group(), v.data(), v.size()), "ComputeGroup::ReadOutput");
+    return v;
+  }
+  void SaveImage(const std::string& path, bool flip_y = true) {
+    const auto img = ReadOutput();
+    check(srt_image_write(path.c_str(), img.data(), w_, h_, flip_y ? 1 : 0), "ComputeGroup::SaveImage");
+  }
+
+ private:
+  void Images() {
+    if (images_dirty_) {
+      check(srt_group_alloc_images(group()), "ComputeGroup: images");
+      images_dirty_ = false;
+    }
+  }
+  std::vector<std::unique_ptr<Compute>> parts_;
+  srt_group* g_ = nullptr;
+  int band_rows_;
+  int w_ = 0, h_ = 0;
+  bool images_dirty_ = true;
 };
 
 }  // namespace Graphics

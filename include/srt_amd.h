@@ -137,6 +137,44 @@ int srt_nan_samples(srt_context* ctx, uint64_t* out);
  * band order.  Default: rank 0 of 1 (whole frame). */
 int srt_set_tiling(srt_context* ctx, int rank, int nranks, int band_rows);
 int srt_local_rows(srt_context* ctx);
+/* The context's HIP device, and a uniform's current value (glGetUniformiv): the int / uint / bool
+ * uniforms above by name; SRT_ERR_NOT_FOUND for other names. */
+int srt_device(srt_context* ctx);
+int srt_get_int(srt_context* ctx, const char* name, int* v);
+
+/* ===================== multi-GPU frame from one host process =====================
+ * The reference's frame loop (src/main.cpp:657-725) drives one GL context.  A C++ embedder tiles the
+ * same frame over the GPUs of a node with a group of contexts, one per device, each holding the scene,
+ * noise and lights (srt_upload_scene etc. on every context): context i renders the row bands b of
+ * `band_rows` rows with b % n == i, with global pixel coordinates; one gather of every context's
+ * radiance rows to context 0 -- ncclGather over xGMI (RCCL, one communicator per device from
+ * ncclCommInitAll) -- then context 0 de-interleaves the bands and encodes sRGB8 (srt_assemble_bands).
+ * The frame is bit-identical to one device's.  A device list that repeats a device (RCCL takes one rank
+ * per device), or SRT_GROUP_TRANSPORT=copy, gathers with device-to-device copies instead.
+ * Contexts stay owned by the caller and must outlive the group. */
+typedef struct srt_group srt_group;
+int srt_group_create(srt_context* const* ctxs, int n, int band_rows, srt_group** out);
+int srt_group_destroy(srt_group* g);
+/* Uniform setters broadcast to every context (the names of srt_set_*). */
+int srt_group_set_bool(srt_group* g, const char* name, int v);
+int srt_group_set_int(srt_group* g, const char* name, int v);
+int srt_group_set_uint(srt_group* g, const char* name, uint32_t v);
+int srt_group_set_vec3(srt_group* g, const char* name, float x, float y, float z);
+/* After Width/Height: tiles the contexts (srt_set_tiling i of n), gives each an equal-size padded band
+ * image (the gather's send buffer) and context 0 the full-frame images. */
+int srt_group_alloc_images(srt_group* g);
+/* glDispatchCompute on every context (srt_dispatch), then the gather and the full-frame assembly
+ * (image0 written unless resetAccumBuffer, as the reference's reset dispatch returns before its store). */
+int srt_group_dispatch(srt_group* g, uint32_t groups_x, uint32_t groups_y);
+/* srt_render_frames on every context, then the gather and the assembly for the last frame. */
+int srt_group_render_frames(srt_group* g, int frame_first, int nframes);
+int srt_group_finish(srt_group* g);  /* glFinish on every device */
+/* The full frame (Width x Height) on the host, or its device pointers on context 0's device. */
+int srt_group_read_accum(srt_group* g, float* host_rgba32f, size_t bytes);
+int srt_group_read_output(srt_group* g, uint8_t* host_rgba8, size_t bytes);
+int srt_group_image_pointers(srt_group* g, void** accum_dev, void** out_dev);
+/* "rccl" or "copy". */
+const char* srt_group_transport(srt_group* g);
 
 /* ===================== bindings (SSBOs / texel buffers / images) ===================== */
 /* AssetUtils::UploadModelDataToGPU (include/asset_utils/gpu_loader.h:19,

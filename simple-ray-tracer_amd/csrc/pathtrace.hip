@@ -763,6 +763,23 @@ int srt_set_tiling(srt_context* c, int rank, int nranks, int band_rows) {
 
 int srt_local_rows(srt_context* c) { return c ? LocalRows(c, c->H) : -1; }
 
+int srt_device(srt_context* c) { return c ? c->device : -1; }
+
+int srt_get_int(srt_context* c, const char* name, int* v) {
+  if (!c || !name || !v) return SRT_ERR_INVALID;
+  const std::string n(name);
+  if (n == "Width") *v = c->W;
+  else if (n == "Height") *v = c->H;
+  else if (n == "accumFrames") *v = c->accum_frames;
+  else if (n == "lightCount") *v = c->light_count;
+  else if (n == "maxDepth") *v = c->max_depth;
+  else if (n == "bvh_count") *v = (int)c->bvh_count;
+  else if (n == "resetAccumBuffer") *v = c->reset;
+  else if (n == "showModel") *v = c->show_model;
+  else return SRT_ERR_NOT_FOUND;
+  return SRT_OK;
+}
+
 int srt_dispatch(srt_context* c, uint32_t gx, uint32_t gy) {
   if (!c) return SRT_ERR_INVALID;
   HIP_OK(hipSetDevice(c->device));

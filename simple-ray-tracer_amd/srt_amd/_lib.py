@@ -108,6 +108,22 @@ _SIGS = {
     "srt_checkpoint_load": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_int32)]),
     "srt_set_tiling": (C.c_int, [P, C.c_int, C.c_int, C.c_int]),
     "srt_local_rows": (C.c_int, [P]),
+    "srt_device": (C.c_int, [P]),
+    "srt_get_int": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_int)]),
+    "srt_group_create": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, C.POINTER(P)]),
+    "srt_group_destroy": (C.c_int, [P]),
+    "srt_group_set_bool": (C.c_int, [P, C.c_char_p, C.c_int]),
+    "srt_group_set_int": (C.c_int, [P, C.c_char_p, C.c_int]),
+    "srt_group_set_uint": (C.c_int, [P, C.c_char_p, C.c_uint32]),
+    "srt_group_set_vec3": (C.c_int, [P, C.c_char_p, C.c_float, C.c_float, C.c_float]),
+    "srt_group_alloc_images": (C.c_int, [P]),
+    "srt_group_dispatch": (C.c_int, [P, C.c_uint32, C.c_uint32]),
+    "srt_group_render_frames": (C.c_int, [P, C.c_int, C.c_int]),
+    "srt_group_finish": (C.c_int, [P]),
+    "srt_group_read_accum": (C.c_int, [P, P, C.c_size_t]),
+    "srt_group_read_output": (C.c_int, [P, P, C.c_size_t]),
+    "srt_group_image_pointers": (C.c_int, [P, C.POINTER(P), C.POINTER(P)]),
+    "srt_group_transport": (C.c_char_p, [P]),
     "srt_upload_scene": (C.c_int, [P, P, C.c_uint32, P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P,
                                    C.c_uint32]),
     "srt_upload_textures": (C.c_int, [P, C.POINTER(Texture), C.c_uint32]),

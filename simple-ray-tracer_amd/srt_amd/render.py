@@ -117,6 +117,96 @@ class Renderer:
         self.compute.close()
 
 
+class GroupRenderer:
+    """One frame tiled over several contexts of this process through the C ABI's device group
+    (srt_group_*: row bands per context, one gather to context 0 -- RCCL across distinct devices, device
+    copies when a device repeats -- and the full-frame assembly).  The same loop as Renderer."""
+
+    def __init__(self, setup: FrameSetup, devices=(0,), *, band_rows: int = 8):
+        import ctypes as C
+
+        from ._lib import check, lib
+
+        self.setup = setup
+        self.parts = [Renderer(setup, device=d) for d in devices]
+        ctxs = (C.c_void_p * len(devices))(*[r.compute.ctx for r in self.parts])
+        g = C.c_void_p()
+        check(lib().srt_group_create(ctxs, len(devices), band_rows, C.byref(g)), "group_create")
+        self.g = g
+        check(lib().srt_group_alloc_images(g), "group_alloc_images")
+        self.accum_frames = 0
+
+    @property
+    def transport(self) -> str:
+        from ._lib import lib
+
+        return lib().srt_group_transport(self.g).decode()
+
+    @property
+    def groups(self):
+        s = self.setup
+        return (s.width + 7) // 8, (s.height + 7) // 8
+
+    def _set(self, reset: bool):
+        from ._lib import check, lib
+
+        check(lib().srt_group_set_bool(self.g, b"resetAccumBuffer", int(reset)), "group_set_bool")
+        check(lib().srt_group_set_int(self.g, b"accumFrames", self.accum_frames), "group_set_int")
+
+    def clear(self):
+        from ._lib import check, lib
+
+        self.accum_frames = 1
+        self._set(True)
+        check(lib().srt_group_dispatch(self.g, *self.groups), "group_dispatch")
+        self._set(False)
+
+    def frame(self):
+        from ._lib import check, lib
+
+        self.accum_frames += 1
+        self._set(False)
+        check(lib().srt_group_dispatch(self.g, *self.groups), "group_dispatch")
+
+    def render(self, spp: int, *, clear: bool = True):
+        from ._lib import check, lib
+
+        if clear:
+            self.clear()
+        check(lib().srt_group_render_frames(self.g, self.accum_frames + 1, spp), "group_render_frames")
+        self.accum_frames += spp
+
+    def finish(self):
+        from ._lib import check, lib
+
+        check(lib().srt_group_finish(self.g), "group_finish")
+
+    def accum(self) -> np.ndarray:
+        from ._lib import check, lib
+
+        s = self.setup
+        a = np.zeros((s.height, s.width, 4), np.float32)
+        check(lib().srt_group_read_accum(self.g, a.ctypes.data, a.nbytes), "group_read_accum")
+        return a
+
+    def output(self) -> np.ndarray:
+        from ._lib import check, lib
+
+        s = self.setup
+        o = np.zeros((s.height, s.width, 4), np.uint8)
+        check(lib().srt_group_read_output(self.g, o.ctypes.data, o.nbytes), "group_read_output")
+        return o
+
+    def close(self):
+        from ._lib import lib
+
+        if self.g is not None:
+            lib().srt_group_destroy(self.g)
+            self.g = None
+        for r in self.parts:
+            r.close()
+
+
 def rubik_model(objects_dir: str | pathlib.Path) -> Model:
     return load_obj(pathlib.Path(objects_dir) / "Rubik" / "Rubik.obj")
 
