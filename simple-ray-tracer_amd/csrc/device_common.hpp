@@ -48,6 +48,11 @@ struct KParams {
   int local_pixels;        // W * local_rows
   int trav_frac16;         // resume shading when fewer than trav_frac16/16 of working lanes traverse
   int bounce_cap;          // bounces after which a path is cut (and counted in ST_BOUNCECAP)
+  // pool_kernel (pool.hpp): LDS byte offsets of the control words, the 3 rings (pool_cap u32 each)
+  // and the pool_slots 112-B records; the hits a shading wave waits for, and the level of the trace
+  // + spare rings under which it shades fewer; the watchdog (s_memrealtime ticks)
+  int pool_ctl_off, pool_ring_off, pool_rec_off, pool_cap, pool_slots, pool_batch, pool_tlow;
+  unsigned long long pool_deadline;
   int stack_base_f4;       // first float4 of the per-lane stacks in dynamic LDS
   uint32_t* gstack;        // global-scene mode: per-lane stacks in HBM, entry field k of lane g at gstack[k * stride + g]
   int gstack_stride;       // lanes in the grid
@@ -74,7 +79,8 @@ enum { ST_RAYS = 0, ST_NODES, ST_TRIS, ST_RNGU, ST_RNGSQ, ST_LIGHTS, ST_MATS, ST
        // lane occupancy of the traversal loop (summed popcounts per iteration) and of shading
        ST_DBG_TITERS, ST_DBG_WORK, ST_DBG_TRAV, ST_DBG_LEAF, ST_DBG_INT, ST_DBG_SHADE,
        // per traversal sub-step k < 16: lanes taking it (summed), waves executing it, lanes popping after it
-       ST_DBG_SUB, ST_TOTAL = ST_DBG_SUB + 48 };
+       ST_DBG_SUB, ST_POOLERR = ST_DBG_SUB + 48,  // pool_kernel's watchdog fired (pool.hpp)
+       ST_TOTAL };
 
 // Diagnostic build only (-DSRT_SUBSTEP_STATS): per-sub-step lane counts (global atomics, slow).
 #ifdef SRT_SUBSTEP_STATS

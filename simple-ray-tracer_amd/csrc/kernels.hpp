@@ -38,6 +38,192 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
 #ifndef SRT_GLOBAL_WAVES
 #define SRT_GLOBAL_WAVES 4
 #endif
+// GetRayColor's loop body for a ray whose CheckHit hit (raytrace_compute.glsl:225-290): the
+// hit record, this bounce's draws, SampleLights, both shadow outcomes of the direct light
+// (q0: occluded, q1: visible), the BRDF choice, Russian roulette and the next direction.
+// `ht`: the hit triangle (mesh scene) or `hit_sphere`; `dist`: the hit distance along (ro, rd).
+// Returns what the path traces next: kShadeShadow (CheckLightOccluded's ray, ro/rd/tmax set,
+// the bounce direction in nd), kShadeBounce (the next CheckHit ray) or kShadeDone.
+enum { kShadeDone = 0, kShadeShadow = 1, kShadeBounce = 2 };
+template <bool COUNT, bool LDSM, bool TEX>
+__device__ __forceinline__ int shade_hit(const KParams& kp, const Lane& ln, Counters& c, uint32_t ht, int hit_sphere,
+                                         float dist, f3& ro, f3& rd, float& tmax, f3& T, int& depth, int& randIndex,
+                                         int& bounces, bool& term, f3& q0, f3& q1, f3& nd) {
+  // ---- hit record (CheckHit) ----
+  Hit rec;
+  rec.hit = true;
+  if (kp.show_model) {
+    rec.p = (dist * rd) + ro;
+    const float4* tp = tri_ptr<LDSM>(kp, ht);
+    const float4 A = tp[0], B = tp[1], C = tp[2];
+    rec.normal = normalize(cross(mk(A.w, B.x, B.y), mk(B.z, B.w, C.x)));
+    const uint32_t mi = __float_as_uint(C.y);
+    float4 m0, m1;
+    if (kp.mats_lds) {
+      m0 = lds4((uint32_t)(kp.mats_base_f4 + 2 * mi) << 4);
+      m1 = lds4((uint32_t)(kp.mats_base_f4 + 2 * mi + 1) << 4);
+    } else {
+      m0 = kp.mats[2 * mi];
+      m1 = kp.mats[2 * mi + 1];
+    }
+    bump<COUNT>(c, ST_MATS);
+    rec.mat.albedo = mk(m0.x, m0.y, m0.z);
+    if constexpr (TEX) {  // the instance for scenes whose materials sample a texture
+      const uint32_t tex = __float_as_uint(m1.w);  // sampled texture + 1
+      if (tex != 0u) rec.mat.albedo = mesh_texture_albedo(kp, tex - 1, ht, A, B, C, dist, ro, rd);
+    }
+    rec.mat.roughness = m0.w;
+    rec.mat.specular = mk(m1.x, m1.y, m1.z);
+    rec.mat.metalness = 0.1f;
+    rec.mat.useSpec = true;
+  } else {
+    f3 pos; float radius;
+    sphere_data(hit_sphere, pos, radius, rec.mat);
+    rec.p = ro + rd * dist;
+    const f3 outward = (rec.p - pos) / radius;   // SetFaceNormal (raytrace_utils.glsl:23-26)
+    rec.normal = (dot(rd, outward) < 0.0f) ? outward : -outward;
+  }
+  const f3 p = rec.p;
+  const f3 Vv = -rd;
+
+  // ---- this bounce's independent uniform draws, fetched together ----
+  const int n = kp.light_count;
+  const bool fixed_spec = (rec.mat.metalness == 1.0f && rec.mat.roughness == 0.0f);
+  const int i_r1 = randU_index(kp, ln, p.x, p.y);             // light index; SampleDiffuse r1
+  const int i_r2 = randU_index(kp, ln, p.y, p.z);             // SampleDiffuse r2
+  const int i_sel = randU_index(kp, ln, p.y + 0.0f, p.z + 0.0f);
+  const int i_bp = randU_index(kp, ln, p.x + (float)depth, p.y + (float)depth);
+  const bool rr = depth <= 0;
+  const int i_rr = rr ? randU_index(kp, ln, p.x + (float)randIndex, p.y + (float)randIndex) : 0;
+  const float r1 = kp.noise_u[i_r1];
+  const float r2 = kp.noise_u[i_r2];
+  const float u_sel0 = kp.noise_u[i_sel];
+  const float u_bp = kp.noise_u[i_bp];
+  const float u_rr = rr ? kp.noise_u[i_rr] : 1.0f;
+  if constexpr (COUNT) c.v[ST_RNGU] += 4 + (rr ? 1 : 0);
+
+  // ---- SampleLights (raytrace_compute.glsl:179-206) ----
+  // randLightIndex uses the same seed every iteration, so the light and its
+  // pdf are loop-invariant; after the first selection later iterations only
+  // re-select it, so their draws are skipped (the result is unchanged).
+  bool selected = false;
+  float lw = 0.0f;
+  LightRec L;
+  f3 toL = mk(0.f, 0.f, 0.f);
+  float fo = 0.0f, d2L = 0.0f;
+  if (n > 0) {
+    L = load_light<COUNT>(kp, c, f2i(__builtin_rintf(r1 * (float)n)));
+    toL = L.pos - p;
+    d2L = dot(toL, toL);
+    fo = recip_exact((0.01f * 0.01f) + d2L);  // GetLightFalloff(p, L) (brdf.glsl:147-152)
+    const float inten = L.intensity * fo;
+    const float lpdf = luminance(mk(inten, inten, inten));
+    const float ris = lpdf * (float)n;
+    // Iteration i selects when its draw r < ris / total_i with total_i =
+    // (i + 1) * ris.  When ris / total is NaN (ris is 0 -- the zero record
+    // past the lights -- or not finite) it is NaN at every i: no draw can
+    // select and the draws are skipped: they never change a value (the
+    // counters count the fetches the kernel makes).  This ~1-in-2n case
+    // otherwise costs n - 1 dependent gathers, and with ~35 shading lanes
+    // nearly every wave has such a lane.
+    float total = ris, pdf = 0.0f;  // 0 + ris
+    if (u_sel0 < (ris / total)) {
+      pdf = lpdf;
+      selected = true;
+    }
+    const bool draws = !selected && (ris / total == ris / total);
+    for (int i = 1; i < n; ++i) {
+      total += ris;
+      if (draws && !selected) {
+        const float r = randU<COUNT>(kp, ln, c, p.y + (float)i, p.z + (float)i);
+        if (r < (ris / total)) {
+          pdf = lpdf;
+          selected = true;
+        }
+      }
+    }
+    lw = (total / (float)n) / fmx(0.001f, pdf);
+  }
+
+  // ---- direct light, both shadow outcomes (raytrace_compute.glsl:233-246) ----
+  f3 sdir = mk(0.f, 0.f, 0.f);
+  float smax = 0.0f;
+  if (selected) {
+    // shared by the shadow ray, getLightData and both direct-light BRDFs:
+    // length(toL), normalize(toL) = toL * (1 / length), light_dir = the
+    // normalized vector (toL itself when zero), the half vector of it and V
+    smax = __builtin_sqrtf(d2L);
+    sdir = toL * recip_exact(smax);
+    const f3 Ld = smax > 0.0f ? sdir : toL;
+    const f3 vl = Vv + Ld;
+    const float lvl = length(vl);
+    const f3 Hn = vl * recip_exact(lvl);  // normalize(vl)
+    if (rec.mat.useSpec) {
+      const float li_ = L.intensity * fo;
+      const f3 bd = sample_direct_brdf(rec, Vv, Ld, lvl > 0.0f ? Hn : vl);
+      q1 = (T * (((1.0f * L.color) * li_) * bd)) * lw;
+      q0 = (T * (((0.0f * L.color) * li_) * bd)) * lw;
+    } else {
+      const f3 lint = ((L.color * fo) * L.intensity) * lw;
+      const f3 tx = T * sample_direct_new(rec, Vv, Ld, Hn);
+      q1 = (tx * 1.0f) * lint;
+      q0 = (tx * 0.0f) * lint;
+    }
+  }
+
+  // ---- BRDF choice, Russian roulette, next direction (:248-285) ----
+  int type;
+  if (fixed_spec) {
+    type = SPECULAR_BRDF;
+  } else {
+    const float bp = brdf_probability(rec.mat, Vv, rec.normal);
+    // T / bp (specular) or T / (1 - bp) (diffuse): one division by the chosen divisor
+    const bool spec = u_bp < bp;
+    type = spec ? SPECULAR_BRDF : DIFFUSE_BRDF;
+    T = T / (spec ? bp : (1.0f - bp));
+  }
+  term = false;
+  if (rr) {
+    const float surv = clampf(luminance(T), 0.1f, 1.0f);
+    if (u_rr > surv) {
+      term = true;
+    } else {
+      T = T / surv;
+      randIndex++;
+    }
+  } else {
+    depth--;
+  }
+  if (!term) {
+    f3 dir, bw;
+    if (!sample_indirect(rec, Vv, type, r1, r2, dir, bw)) {
+      term = true;
+    } else {
+      T = T * bw;
+      nd = dir;
+    }
+  }
+
+  // The reference's loop has no depth cap (Russian roulette clamps the
+  // survival probability to >= 0.1).  A path still alive after
+  // kp.bounce_cap bounces (2^20 unless SRT_BOUNCE_CAP says otherwise) is
+  // cut and counted, so a pathological scene cannot hang the GPU.
+  if (++bounces >= kp.bounce_cap && !term) {
+    term = true;
+    bump<COUNT>(c, ST_BOUNCECAP);
+  }
+  ro = p;
+  if (selected) {  // trace CheckLightOccluded's ray next (t in (0.001, |light - p|))
+    rd = sdir;
+    tmax = smax;
+    return kShadeShadow;
+  }
+  if (term) return kShadeDone;
+  rd = nd;
+  tmax = __builtin_inff();
+  return kShadeBounce;
+}
+
 // waves per SIMD the register allocation must allow: 4 (<= 128 VGPRs) in LDS
 // mode, where the 1024-thread block's LDS caps residency at 4 anyway;
 // SRT_GLOBAL_WAVES in global-scene mode, whose HBM latency wants more waves
@@ -295,181 +481,12 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
       } else if (!hit) {
         finish_sample();
       } else {
-        // ---- hit record (CheckHit) ----
-        Hit rec;
-        rec.hit = true;
-        if (kp.show_model) {
-          rec.p = (dist * rd) + ro;
-          const uint32_t ht = tr.hit;
-          const float4* tp = tri_ptr<LDSM>(kp, ht);
-          const float4 A = tp[0], B = tp[1], C = tp[2];
-          rec.normal = normalize(cross(mk(A.w, B.x, B.y), mk(B.z, B.w, C.x)));
-          const uint32_t mi = __float_as_uint(C.y);
-          float4 m0, m1;
-          if (kp.mats_lds) {
-            m0 = lds4((uint32_t)(kp.mats_base_f4 + 2 * mi) << 4);
-            m1 = lds4((uint32_t)(kp.mats_base_f4 + 2 * mi + 1) << 4);
-          } else {
-            m0 = kp.mats[2 * mi];
-            m1 = kp.mats[2 * mi + 1];
-          }
-          bump<COUNT>(c, ST_MATS);
-          rec.mat.albedo = mk(m0.x, m0.y, m0.z);
-          if constexpr (TEX) {  // the instance for scenes whose materials sample a texture
-            const uint32_t tex = __float_as_uint(m1.w);  // sampled texture + 1
-            if (tex != 0u) rec.mat.albedo = mesh_texture_albedo(kp, tex - 1, ht, A, B, C, dist, ro, rd);
-          }
-          rec.mat.roughness = m0.w;
-          rec.mat.specular = mk(m1.x, m1.y, m1.z);
-          rec.mat.metalness = 0.1f;
-          rec.mat.useSpec = true;
-        } else {
-          f3 pos; float radius;
-          sphere_data(hit_sphere, pos, radius, rec.mat);
-          rec.p = ro + rd * dist;
-          const f3 outward = (rec.p - pos) / radius;   // SetFaceNormal (raytrace_utils.glsl:23-26)
-          rec.normal = (dot(rd, outward) < 0.0f) ? outward : -outward;
-        }
-        const f3 p = rec.p;
-        const f3 Vv = -rd;
-
-        // ---- this bounce's independent uniform draws, fetched together ----
-        const int n = kp.light_count;
-        const bool fixed_spec = (rec.mat.metalness == 1.0f && rec.mat.roughness == 0.0f);
-        const int i_r1 = randU_index(kp, ln, p.x, p.y);             // light index; SampleDiffuse r1
-        const int i_r2 = randU_index(kp, ln, p.y, p.z);             // SampleDiffuse r2
-        const int i_sel = randU_index(kp, ln, p.y + 0.0f, p.z + 0.0f);
-        const int i_bp = randU_index(kp, ln, p.x + (float)depth, p.y + (float)depth);
-        const bool rr = depth <= 0;
-        const int i_rr = rr ? randU_index(kp, ln, p.x + (float)randIndex, p.y + (float)randIndex) : 0;
-        const float r1 = kp.noise_u[i_r1];
-        const float r2 = kp.noise_u[i_r2];
-        const float u_sel0 = kp.noise_u[i_sel];
-        const float u_bp = kp.noise_u[i_bp];
-        const float u_rr = rr ? kp.noise_u[i_rr] : 1.0f;
-        if constexpr (COUNT) c.v[ST_RNGU] += 4 + (rr ? 1 : 0);
-
-        // ---- SampleLights (raytrace_compute.glsl:179-206) ----
-        // randLightIndex uses the same seed every iteration, so the light and its
-        // pdf are loop-invariant; after the first selection later iterations only
-        // re-select it, so their draws are skipped (the result is unchanged).
-        bool selected = false;
-        float lw = 0.0f;
-        LightRec L;
-        f3 toL = mk(0.f, 0.f, 0.f);
-        float fo = 0.0f, d2L = 0.0f;
-        if (n > 0) {
-          L = load_light<COUNT>(kp, c, f2i(__builtin_rintf(r1 * (float)n)));
-          toL = L.pos - p;
-          d2L = dot(toL, toL);
-          fo = recip_exact((0.01f * 0.01f) + d2L);  // GetLightFalloff(p, L) (brdf.glsl:147-152)
-          const float inten = L.intensity * fo;
-          const float lpdf = luminance(mk(inten, inten, inten));
-          const float ris = lpdf * (float)n;
-          // Iteration i selects when its draw r < ris / total_i with total_i =
-          // (i + 1) * ris.  When ris / total is NaN (ris is 0 -- the zero record
-          // past the lights -- or not finite) it is NaN at every i: no draw can
-          // select and the draws are skipped: they never change a value (the
-          // counters count the fetches the kernel makes).  This ~1-in-2n case
-          // otherwise costs n - 1 dependent gathers, and with ~35 shading lanes
-          // nearly every wave has such a lane.
-          float total = ris, pdf = 0.0f;  // 0 + ris
-          if (u_sel0 < (ris / total)) {
-            pdf = lpdf;
-            selected = true;
-          }
-          const bool draws = !selected && (ris / total == ris / total);
-          for (int i = 1; i < n; ++i) {
-            total += ris;
-            if (draws && !selected) {
-              const float r = randU<COUNT>(kp, ln, c, p.y + (float)i, p.z + (float)i);
-              if (r < (ris / total)) {
-                pdf = lpdf;
-                selected = true;
-              }
-            }
-          }
-          lw = (total / (float)n) / fmx(0.001f, pdf);
-        }
-
-        // ---- direct light, both shadow outcomes (raytrace_compute.glsl:233-246) ----
-        f3 sdir = mk(0.f, 0.f, 0.f);
-        float smax = 0.0f;
-        if (selected) {
-          // shared by the shadow ray, getLightData and both direct-light BRDFs:
-          // length(toL), normalize(toL) = toL * (1 / length), light_dir = the
-          // normalized vector (toL itself when zero), the half vector of it and V
-          smax = __builtin_sqrtf(d2L);
-          sdir = toL * recip_exact(smax);
-          const f3 Ld = smax > 0.0f ? sdir : toL;
-          const f3 vl = Vv + Ld;
-          const float lvl = length(vl);
-          const f3 Hn = vl * recip_exact(lvl);  // normalize(vl)
-          if (rec.mat.useSpec) {
-            const float li_ = L.intensity * fo;
-            const f3 bd = sample_direct_brdf(rec, Vv, Ld, lvl > 0.0f ? Hn : vl);
-            q1 = (T * (((1.0f * L.color) * li_) * bd)) * lw;
-            q0 = (T * (((0.0f * L.color) * li_) * bd)) * lw;
-          } else {
-            const f3 lint = ((L.color * fo) * L.intensity) * lw;
-            const f3 tx = T * sample_direct_new(rec, Vv, Ld, Hn);
-            q1 = (tx * 1.0f) * lint;
-            q0 = (tx * 0.0f) * lint;
-          }
-        }
-
-        // ---- BRDF choice, Russian roulette, next direction (:248-285) ----
-        int type;
-        if (fixed_spec) {
-          type = SPECULAR_BRDF;
-        } else {
-          const float bp = brdf_probability(rec.mat, Vv, rec.normal);
-          // T / bp (specular) or T / (1 - bp) (diffuse): one division by the chosen divisor
-          const bool spec = u_bp < bp;
-          type = spec ? SPECULAR_BRDF : DIFFUSE_BRDF;
-          T = T / (spec ? bp : (1.0f - bp));
-        }
-        term = false;
-        if (rr) {
-          const float surv = clampf(luminance(T), 0.1f, 1.0f);
-          if (u_rr > surv) {
-            term = true;
-          } else {
-            T = T / surv;
-            randIndex++;
-          }
-        } else {
-          depth--;
-        }
-        if (!term) {
-          f3 dir, bw;
-          if (!sample_indirect(rec, Vv, type, r1, r2, dir, bw)) {
-            term = true;
-          } else {
-            T = T * bw;
-            nd = dir;
-          }
-        }
-
-        // The reference's loop has no depth cap (Russian roulette clamps the
-        // survival probability to >= 0.1).  A path still alive after
-        // kp.bounce_cap bounces (2^20 unless SRT_BOUNCE_CAP says otherwise) is
-        // cut and counted, so a pathological scene cannot hang the GPU.
-        if (++bounces >= kp.bounce_cap && !term) {
-          term = true;
-          bump<COUNT>(c, ST_BOUNCECAP);
-        }
-        ro = p;
-        if (selected) {  // trace CheckLightOccluded's ray next (t in (0.001, |light - p|))
-          rd = sdir;
-          tmax = smax;
-          shadow_phase = true;
-          pending = true;  // started with the refill's new rays (one start_ray pass)
-        } else if (term) {
+        const int next = shade_hit<COUNT, LDSM, TEX>(kp, ln, c, tr.hit, hit_sphere, dist, ro, rd, tmax, T, depth,
+                                                     randIndex, bounces, term, q0, q1, nd);
+        if (next == kShadeDone) {
           finish_sample();
         } else {
-          rd = nd;
-          tmax = __builtin_inff();
+          shadow_phase = next == kShadeShadow;
           pending = true;  // started with the refill's new rays (one start_ray pass)
         }
       }

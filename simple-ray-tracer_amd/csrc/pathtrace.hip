@@ -36,6 +36,7 @@
 #include <zlib.h>
 
 #include "kernels.hpp"
+#include "pool.hpp"
 
 // ===========================================================================
 // host side: the device context behind the C ABI
@@ -130,7 +131,13 @@ struct srt_context {
   int tail_claims = 16;  // SRT_TAIL_CLAIMS: claims per wave before the end from which claims take one batch
   int trav_frac16 = 9;                 // SRT_TRAV_FRAC16 (measured best on Rubik 1080p with the 16-sub-step pattern)
   int bounce_cap = 1 << 20;            // SRT_BOUNCE_CAP: bounces after which a path is cut (counted)
-  int trav_frac16_global = 9;          // SRT_TRAV_FRAC16_GLOBAL: the same threshold for global-scene mode
+  int trav_frac16_global = 9;
+  bool pool_launched = false;          // the last render ran pool_kernel (srt_finish checks its watchdog)
+  int pool = 0;                        // SRT_POOL=1: LDS mode runs pool_kernel (workgroup ray pools)
+  int pool_batch = 64;                 // SRT_POOL_BATCH: queued hits a shading wave waits for
+  int pool_tlow = 32;                  // SRT_POOL_TLOW: trace + spare records under which shading waves take fewer
+  int pool_slots_max = 4096;           // SRT_POOL_SLOTS: at most this many records
+  int pool_deadline_ms = 30000;        // SRT_POOL_DEADLINE_MS: pool_kernel's watchdog          // SRT_TRAV_FRAC16_GLOBAL: the same threshold for global-scene mode
   int num_cus = 256;
   // stats
   unsigned long long* d_stats = nullptr;
@@ -387,6 +394,20 @@ int LaunchMode(srt_context* c, const srt::KParams& kc, size_t lds, bool count, b
               : LaunchSamples<false, false, false, 256, TEX>(c, kc, lds);
 }
 
+// pool_kernel (pool.hpp): one 1024-thread block per CU, as sample_kernel's LDS mode.
+template <bool COUNT>
+int LaunchPool(srt_context* c, srt::KParams kp, size_t lds) {
+  const int blocks = c->num_cus;
+  kp.tail_start = (int)std::max<long long>(
+      0, (long long)((kp.W + 7) >> 3) * ((kp.local_rows + 7) >> 3) * kp.nframes -
+             (long long)c->tail_claims * srt::kClaim * blocks * srt::kPoolTravWaves);
+  HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
+  hipLaunchKernelGGL(srt::pool_kernel<COUNT>, dim3(blocks), dim3(1024), lds, c->stream, kp);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
+  return SRT_OK;
+}
+
 // Runs frames kp.frame_first .. + kp.nframes - 1 (or the reset frame) through
 // sample_kernel + accumulate_kernel, in chunks that fit the sample buffer.
 int Launch(srt_context* c, srt::KParams& kp, bool count) {
@@ -405,29 +426,64 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   const size_t lds_mode_bytes = scene_bytes + (size_t)1024 * 2 * sizeof(uint32_t) * (size_t)kp.stack_entries;
   const bool ldsm = kp.show_model && c->lds_ok && c->pairs_aligned && !c->force_global && lds_mode_bytes <= kLdsBytes;
   const int block = ldsm ? 1024 : 256;
-  size_t lds;
-  if (ldsm) {
-    kp.stack_base_f4 = kp.nodes_lds_f4 + kp.tris_f4;
-    lds = lds_mode_bytes;
-  } else {  // LDS rings of kShortStack entries per lane, backed by HBM stacks (LaunchSamples)
-    kp.stack_base_f4 = 0;
-    lds = (size_t)block * (c->lds_ok ? 2 : 3) * sizeof(uint32_t) * (size_t)srt::kShortStack;
-  }
-  {  // light and material records in LDS behind the rest, when they fit (shading reads them there)
-    lds = (lds + 15) & ~(size_t)15;
-    const size_t light_bytes = 2 * sizeof(float4) * ((size_t)kp.light_records + 1);
-    kp.lights_lds = (light_bytes <= 8192 && lds + light_bytes <= kLdsBytes) ? 1 : 0;
-    if (kp.lights_lds) {
-      kp.lights_base_f4 = (int)(lds / sizeof(float4));
-      lds += light_bytes;
+  // pool mode (pool.hpp): LDS mode with stacks for the traversal waves only, then the ray records;
+  // laid out first, and sample_kernel's layout when the records do not fit
+  bool pool = ldsm && c->pool && !c->sample_textures && kp.max_depth >= 0 && kp.max_depth <= 255;
+  size_t lds = 0;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    if (pool) {
+      kp.stack_base_f4 = kp.nodes_lds_f4 + kp.tris_f4;
+      lds = scene_bytes + (size_t)srt::kPoolTravLanes * 2 * sizeof(uint32_t) * (size_t)kp.stack_entries;
+    } else if (ldsm) {
+      kp.stack_base_f4 = kp.nodes_lds_f4 + kp.tris_f4;
+      lds = lds_mode_bytes;
+    } else {  // LDS rings of kShortStack entries per lane, backed by HBM stacks (LaunchSamples)
+      kp.stack_base_f4 = 0;
+      lds = (size_t)block * (c->lds_ok ? 2 : 3) * sizeof(uint32_t) * (size_t)srt::kShortStack;
     }
-    kp.mat_records = (int)c->n_mats + 1;
-    const size_t mat_bytes = 2 * sizeof(float4) * (size_t)kp.mat_records;
-    kp.mats_lds = (kp.show_model && c->d_mats && mat_bytes <= 16384 && lds + mat_bytes <= kLdsBytes) ? 1 : 0;
-    if (kp.mats_lds) {
-      kp.mats_base_f4 = (int)(lds / sizeof(float4));
-      lds += mat_bytes;
+    {  // light and material records in LDS behind the rest, when they fit (shading reads them there)
+      lds = (lds + 15) & ~(size_t)15;
+      const size_t light_bytes = 2 * sizeof(float4) * ((size_t)kp.light_records + 1);
+      kp.lights_lds = (light_bytes <= 8192 && lds + light_bytes <= kLdsBytes) ? 1 : 0;
+      if (kp.lights_lds) {
+        kp.lights_base_f4 = (int)(lds / sizeof(float4));
+        lds += light_bytes;
+      }
+      kp.mat_records = (int)c->n_mats + 1;
+      const size_t mat_bytes = 2 * sizeof(float4) * (size_t)kp.mat_records;
+      kp.mats_lds = (kp.show_model && c->d_mats && mat_bytes <= 16384 && lds + mat_bytes <= kLdsBytes) ? 1 : 0;
+      if (kp.mats_lds) {
+        kp.mats_base_f4 = (int)(lds / sizeof(float4));
+        lds += mat_bytes;
+      }
     }
+    if (!pool) break;
+    // control words, 3 rings of u32 record ids (power-of-two capacity), 112-B records
+    kp.pool_ctl_off = (int)lds;
+    lds += 16 * sizeof(uint32_t);
+    int slots = 0, cap = 1;
+    for (int r = std::min(c->pool_slots_max, 65534); r >= 64 && slots == 0; --r) {
+      int cp = 1;
+      while (cp < r) cp <<= 1;
+      if (lds + (size_t)3 * cp * sizeof(uint32_t) + (size_t)r * 112 <= kLdsBytes) {
+        slots = r;
+        cap = cp;
+      }
+    }
+    if (slots == 0) {  // no room for 64 records
+      pool = false;
+      continue;
+    }
+    kp.pool_ring_off = (int)lds;
+    lds += (size_t)3 * cap * sizeof(uint32_t);
+    kp.pool_rec_off = (int)lds;
+    lds += (size_t)slots * 112;
+    kp.pool_cap = cap;
+    kp.pool_slots = slots;
+    kp.pool_batch = c->pool_batch;
+    kp.pool_tlow = c->pool_tlow;
+    kp.pool_deadline = (unsigned long long)c->pool_deadline_ms * 100000ull;  // s_memrealtime runs at 100 MHz
+    break;
   }
   // sample buffer: as many frames per chunk as the buffer cap allows
   const size_t per_frame = (size_t)npx * sizeof(float4);
@@ -498,9 +554,11 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
     int rc;
     // LDS mode: packed entries (lds_ok); global-scene mode: packed when indices fit 24 bits
     const bool pack = c->lds_ok;
-    rc = c->sample_textures ? LaunchMode<true>(c, kc, lds, count, ldsm, pack)
-                            : LaunchMode<false>(c, kc, lds, count, ldsm, pack);
+    if (pool) rc = count ? LaunchPool<true>(c, kc, lds) : LaunchPool<false>(c, kc, lds);
+    else rc = c->sample_textures ? LaunchMode<true>(c, kc, lds, count, ldsm, pack)
+                                 : LaunchMode<false>(c, kc, lds, count, ldsm, pack);
     if (rc) return rc;
+    c->pool_launched |= pool;
     c->ev_used += 2;  // LaunchSamples recorded the pair around the launch
     hipLaunchKernelGGL(srt::accumulate_kernel, pgrid, dim3(256), 0, c->stream, kc, out_frames);
     HIP_OK(hipGetLastError());
@@ -650,6 +708,11 @@ int srt_create(int device, void* stream, srt_context** out) {
   if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_MB")) c->lbuf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
   if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_KB")) c->lbuf_cap = (size_t)std::max(1L, std::atol(e)) << 10;
   if (const char* e = std::getenv("SRT_BOUNCE_CAP")) c->bounce_cap = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("SRT_POOL")) c->pool = e[0] == '1';
+  if (const char* e = std::getenv("SRT_POOL_BATCH")) c->pool_batch = std::max(1, std::min(64, std::atoi(e)));
+  if (const char* e = std::getenv("SRT_POOL_TLOW")) c->pool_tlow = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("SRT_POOL_SLOTS")) c->pool_slots_max = std::max(64, std::atoi(e));
+  if (const char* e = std::getenv("SRT_POOL_DEADLINE_MS")) c->pool_deadline_ms = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("SRT_TAIL_CLAIMS")) c->tail_claims = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("SRT_TILE_ORDER")) c->tile_schedule = e[0] != '0';
   if (const char* e = std::getenv("SRT_TRAV_FRAC16")) c->trav_frac16 = std::max(0, std::min(16, std::atoi(e)));
@@ -818,6 +881,15 @@ int srt_render_frames(srt_context* c, int frame_first, int nframes, int write_ou
 int srt_finish(srt_context* c) {
   if (!c) return SRT_ERR_INVALID;
   HIP_OK(hipStreamSynchronize(c->stream));
+  if (c->pool_launched) {  // pool_kernel's watchdog (pool.hpp): a launch that overran its deadline
+    unsigned long long err = 0;
+    HIP_OK(hipMemcpy(&err, c->d_stats + srt::ST_POOLERR, sizeof(err), hipMemcpyDeviceToHost));
+    c->pool_launched = false;
+    if (err) {
+      srt::SetError("pool_kernel: watchdog expired (the render is incomplete)");
+      return SRT_ERR_HIP;
+    }
+  }
   return SRT_OK;
 }
 
