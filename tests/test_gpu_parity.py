@@ -481,3 +481,49 @@ def test_reference_upload_path_renders_oracle_frame(rubik, tmp_path):
     setup.scene.bvhs[1]["frame"] = frame.reshape(16)
     want, _, _ = oracle_render(setup, 3)
     assert bits_equal(acc, want).all()
+
+
+# ---- pool_kernel (pool.hpp, SRT_POOL=1): LDS mode with workgroup ray pools ----
+@pytest.mark.parametrize("w,h,spp,depth", [(64, 64, 2, 5), (96, 54, 4, 5), (31, 23, 3, 8), (40, 72, 2, 0)])
+def test_pool_kernel_parity(rubik, monkeypatch, w, h, spp, depth):
+    """The pool kernel (hits shaded by shading waves from LDS records) renders the oracle's frame, with
+    the counting instance's CheckHit counts, in the fused and the per-frame dispatch paths."""
+    monkeypatch.setenv("SRT_POOL", "1")
+    monkeypatch.setenv("SRT_POOL_DEADLINE_MS", "20000")
+    setup = R.make_setup(w, h, show_model=True, models=[rubik], max_depth=depth)
+    assert_parity(setup, spp)
+    assert_parity(setup, spp, per_frame=True)
+
+
+def test_pool_kernel_scenes_and_tiling(rubik, monkeypatch):
+    """Pool mode on two models with a moved second one (BVH switches inside traversal lanes), a
+    multi-rank band split and small pool batches / record counts: every frame is the oracle's."""
+    monkeypatch.setenv("SRT_POOL", "1")
+    monkeypatch.setenv("SRT_POOL_DEADLINE_MS", "20000")
+    second = S.load_obj(OBJECTS / "Rubik" / "Rubik.obj")
+    two = R.make_setup(48, 40, show_model=True, models=[rubik, second])
+    frame = np.eye(4, dtype=np.float32)
+    frame[3, :3] = (12.0, -2.0, -5.0)
+    two.scene.bvhs[1]["frame"] = frame.reshape(16)
+    assert_parity(two, 2)
+    monkeypatch.setenv("SRT_POOL_BATCH", "8")
+    monkeypatch.setenv("SRT_POOL_SLOTS", "64")
+    setup = R.make_setup(64, 48, show_model=True, models=[rubik])
+    acc, out = assert_parity(setup, 3)
+    parts = [gpu_render(setup, 3, rank=r, nranks=3, band_rows=8)[0] for r in range(3)]
+    from srt_amd import parallel as PAR
+
+    rows_pad = PAR.rows_pad(48, 8, 3)
+    stacked = np.zeros((3, rows_pad, 64, 4), np.float32)
+    for r, p in enumerate(parts):
+        stacked[r, :len(p)] = p
+    assert bits_equal(PAR.assemble_host(stacked, 48, 8), acc).all()
+
+
+def test_pool_kernel_metric_frame_equals_sample_kernel(rubik, monkeypatch):
+    """The metric frame (1920x1080) at 16 spp: pool mode's accumulation and image equal sample_kernel's."""
+    setup = R.make_setup(1920, 1080, show_model=True, models=[rubik])
+    a, o, st = gpu_render(setup, 16)
+    monkeypatch.setenv("SRT_POOL", "1")
+    b, p, st2 = gpu_render(setup, 16)
+    assert bits_equal(a, b).all() and (o == p).all() and st["rays"] == st2["rays"]
