@@ -122,8 +122,9 @@ def cpu_baseline(setup, spp_first: int, target_s: float) -> dict:
     rays = st["rays"] + st2["rays"]
     secs = (t1 - t0) + (t3 - t2)
     return {"value": rays / secs / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"oracle on {len(rows)} rows (every 8th) x {s.width} px x {frames + 1} frames of the same "
-                      f"workload ({rays} rays, {secs:.1f} s)"}
+            "sample": f"oracle (gcc -O2 -mfma -ffp-contract=off: hardware FMA, OpenMP over rows) on {len(rows)} rows "
+                      f"(every 8th) x {s.width} px x {frames + 1} frames of the same workload ({rays} rays, "
+                      f"{secs:.1f} s)"}
 
 
 def load_counters(workload: str):
