@@ -323,10 +323,21 @@ def run_leg(setup, spp, args, *, rank, world, device, stream):
     return float(elapsed.item()), total_rays, st, kernel_ms, run
 
 
-KERNEL_LDS = "srt::sample_kernel<false, true, true, 1024, false, false> (LDS-resident scene)"
-# global-scene mode: fused sub-steps for trees under 600 MB (both legs), the IL pattern past it (C5)
-KERNEL_GLOBAL = "srt::sample_kernel<false, false, true, 256, false, true> (global-scene mode, fused sub-steps)"
-KERNEL_GLOBAL_IL = "srt::sample_kernel<false, false, true, 256, false, false> (global-scene mode, IL sub-steps)"
+KERNEL_LDS = "srt::sample_kernel<false, true, true, 1024, false, false, 4> (LDS-resident scene)"
+
+
+def timed_kernel(run, scene: str) -> str:
+    """The sample_kernel instance the run's timed launches took.  Global-scene mode: fused sub-steps for
+    trees under 600 MB (both legs), the IL pattern past it (C5); the fused instance at 5 waves per SIMD
+    for trees under 48 MB (the surface-mesh leg), else 4 (srt_get_int's scene.* names)."""
+    if scene == "rubik":
+        return KERNEL_LDS
+    if scene == "spheres":
+        return "srt::sample_kernel<false, false, true, 256, false, false, 4> (spheres: no BVH)"
+    fused = run.c.GetInt("scene.fused") == 1
+    gw = run.c.GetInt("scene.global_waves") if fused else 4
+    return (f"srt::sample_kernel<false, false, true, 256, false, {'true' if fused else 'false'}, {gw}> "
+            f"(global-scene mode, {'fused' if fused else 'IL'} sub-steps, {gw} waves per SIMD)")
 
 
 def main(argv=None):
@@ -358,6 +369,7 @@ def main(argv=None):
     if args.dump and rank == 0:
         acc, out = run.frame()
         np.savez(args.dump, accum=acc, out=out)
+    kname = timed_kernel(run, args.scene)
     run.close()
 
     legs = []
@@ -365,6 +377,7 @@ def main(argv=None):
         gsetup, gname = build_setup("synthetic", 1920, 1080, args.global_spp, 5, args.global_tris)
         g_el, g_rays, g_st, g_kms, g_run = run_leg(gsetup, args.global_spp, args, rank=rank, world=world,
                                                    device=device, stream=stream)
+        g_kname = timed_kernel(g_run, "synthetic")
         g_run.close()
         if rank == 0:
             g_k = float(np.mean(g_kms))
@@ -373,7 +386,7 @@ def main(argv=None):
                 "unit": "Mrays/s", "ms_per_step": round(g_el * 1e3 / args.steps, 3),
                 "config": {"scene": f"synthetic {args.global_tris} triangles (SURVEY 8d generator)", "width": 1920,
                            "height": 1080, "spp": args.global_spp, "max_depth": 5},
-                "roofline": roofline(gname, g_k, algorithmic_bytes(g_st) if world == 1 else 0, KERNEL_GLOBAL,
+                "roofline": roofline(gname, g_k, algorithmic_bytes(g_st) if world == 1 else 0, g_kname,
                                      global_mode=True),
             })
 
@@ -381,6 +394,7 @@ def main(argv=None):
         ssetup, sname = build_setup("torusknot", 1920, 1080, args.surface_spp, 5, 0)
         s_el, s_rays, s_st, s_kms, s_run = run_leg(ssetup, args.surface_spp, args, rank=rank, world=world,
                                                    device=device, stream=stream)
+        s_kname = timed_kernel(s_run, "torusknot")
         s_run.close()
         if rank == 0:
             legs.append({
@@ -390,15 +404,13 @@ def main(argv=None):
                                     "torus_knot_triangles), model camera and lights", "width": 1920, "height": 1080,
                            "spp": args.surface_spp, "max_depth": 5},
                 "roofline": roofline(sname, float(np.mean(s_kms)), algorithmic_bytes(s_st) if world == 1 else 0,
-                                     KERNEL_GLOBAL, global_mode=True),
+                                     s_kname, global_mode=True),
             })
 
     if rank == 0:
         ms_per_step = elapsed_s * 1e3 / args.steps
         value = total_rays * args.steps / elapsed_s / 1e6
         k_ms = float(np.mean(kernel_ms))
-        kname = {"rubik": KERNEL_LDS, "synthetic": KERNEL_GLOBAL if args.synthetic_tris * 112 < 600 << 20
-                 else KERNEL_GLOBAL_IL}.get(args.scene, "srt::sample_kernel<false, ...>")
         line = {
             "metric": "Mrays/s (CheckHit queries: camera + bounce + shadow rays) at the BASELINE frame/spp",
             "value": round(value, 3),
@@ -425,7 +437,7 @@ def main(argv=None):
             "rays_per_step": int(total_rays),
             "code_hash": code_hash(),
             # per-rank counters describe rank 0's launch: the roofline is a 1-GPU figure
-            "roofline": roofline(wl_name, k_ms, algorithmic_bytes(st), kname, global_mode=args.scene == "synthetic")
+            "roofline": roofline(wl_name, k_ms, algorithmic_bytes(st), kname, global_mode=args.scene in ("synthetic", "torusknot"))
             if world == 1 else
             {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
              "kernel_ms": round(k_ms, 3), "note": "roofline reported at N=1"},

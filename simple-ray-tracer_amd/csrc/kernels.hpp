@@ -35,9 +35,11 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
 #define SRT_TILE_SCHED 1  // tiles of each frame in the last launch's cost order
 #endif
 
-#ifndef SRT_GLOBAL_WAVES
-#define SRT_GLOBAL_WAVES 4
-#endif
+// Global-scene mode's occupancy regimes (GW, waves per SIMD): 4 (<= 128 VGPRs, no
+// spills; 16-entry LDS rings, 32 KiB per 256-lane block), or 5 (<= 96 VGPRs, ~10
+// dwords spilled; 8-entry rings, 16 KiB per block) for trees small enough that
+// more rays in flight beat the spills (srt_upload_scene picks it by scene size).
+__host__ __device__ constexpr int global_ring(int gw) { return gw > 4 ? 8 : kShortStack; }
 // GetRayColor's loop body for a ray whose CheckHit hit (raytrace_compute.glsl:225-290): the
 // hit record, this bounce's draws, SampleLights, both shadow outcomes of the direct light
 // (q0: occluded, q1: visible), the BRDF choice, Russian roulette and the next direction.
@@ -225,11 +227,11 @@ __device__ __forceinline__ int shade_hit(const KParams& kp, const Lane& ln, Coun
 }
 
 // waves per SIMD the register allocation must allow: 4 (<= 128 VGPRs) in LDS
-// mode, where the 1024-thread block's LDS caps residency at 4 anyway;
-// SRT_GLOBAL_WAVES in global-scene mode, whose HBM latency wants more waves
+// mode, where the 1024-thread block's LDS caps residency at 4 anyway; GW in
+// global-scene mode (see global_ring), whose memory latency wants more waves
 // FUSE: global-scene mode's fused sub-steps (trav_fused) instead of kStepPattern
-template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX, bool FUSE>
-__global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_kernel(KParams kp) {
+template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX, bool FUSE, int GW = 4>
+__global__ __launch_bounds__(BLOCK, LDSM ? 4 : GW) void sample_kernel(KParams kp) {
   const int tid = threadIdx.x;
 #ifdef SRT_WAVE_TRACE
   const unsigned long long tw0 = __builtin_amdgcn_s_memrealtime();
@@ -254,7 +256,7 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
   if constexpr (LDSM) {
     ln.stk = reinterpret_cast<uint32_t*>(g_smem + kp.stack_base_f4) + tid;
     ln.stride = BLOCK;  // a compile-time stride: stack addressing by shifts, no v_mul_lo_u32
-  } else {  // the top kShortStack entries in an LDS ring, the rest in HBM (lane-interleaved, coalesced)
+  } else {  // the top global_ring(GW) entries in an LDS ring, the rest in HBM (lane-interleaved, coalesced)
     ln.stk = reinterpret_cast<uint32_t*>(g_smem) + tid;
     ln.stride = BLOCK;
     ln.gstk = kp.gstack + (size_t)blockIdx.x * BLOCK + tid;
@@ -456,7 +458,7 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : SRT_GLOBAL_WAVES) void sample_ker
         d_leaf += __popcll(__ballot(tr.active && trav_at_leaf(tr.cnt)));
         d_int += __popcll(__ballot(tr.active && tr.cnt == 0));
 #endif
-        if (tr.active) trav_step<COUNT, LDSM, PACK, FUSE>(kp, ln, c, tr, ro, rd, shadow_phase);
+        if (tr.active) trav_step<COUNT, LDSM, PACK, FUSE, global_ring(GW)>(kp, ln, c, tr, ro, rd, shadow_phase);
       }
     }
 

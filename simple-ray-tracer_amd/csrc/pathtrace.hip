@@ -100,6 +100,7 @@ struct srt_context {
   bool pairs_aligned = false; // every internal node's child pair starts at an odd slot (LDS mode's node_pair)
   bool force_global = false;  // SRT_FORCE_GLOBAL_SCENE=1 disables LDS mode
   bool fused = false;         // global-scene mode's fused sub-steps (set at upload: trees the Infinity Cache holds)
+  int global_waves = 4;       // the fused instance's waves per SIMD (set at upload: 5 for small trees)
   // lights
   std::vector<srt_light> h_lights;
   float4* d_lights = nullptr;
@@ -326,16 +327,16 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
 // LDS budget per CU (gfx950: 160 KiB; one 1024-thread block per CU in LDS mode)
 constexpr size_t kLdsBytes = 160 * 1024;
 
-template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX, bool FUSE = false>
+template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX, bool FUSE = false, int GW = 4>
 int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
   // resident blocks per CU, queried once per (kernel instance, LDS size): the
   // query runs on the host between the launch's timing events otherwise
-  const void* fn = reinterpret_cast<const void*>(&srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX, FUSE>);
+  const void* fn = reinterpret_cast<const void*>(&srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX, FUSE, GW>);
   int per_cu = 0;
   for (const auto& e : c->occupancy)
     if (e.fn == fn && e.lds == lds) per_cu = e.per_cu;
   if (per_cu == 0) {
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX, FUSE>,
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX, FUSE, GW>,
                                                           BLOCK, lds));
     per_cu = std::max(per_cu, 1);
     c->occupancy.push_back({fn, lds, per_cu});
@@ -373,14 +374,16 @@ int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
     kp.tail_start = (int)std::max<long long>(0, n_batches - (long long)c->tail_claims * srt::kClaim * waves);
   }
   HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
-  hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX, FUSE>), dim3(blocks), dim3(BLOCK), lds, c->stream, kp);
+  hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX, FUSE, GW>), dim3(blocks), dim3(BLOCK), lds, c->stream,
+                     kp);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
   return SRT_OK;
 }
 
 // The sample_kernel instance for the launch: counting or not, LDS-resident
-// scene or global (packed stack entries when indices fit 24 bits), and with
+// scene or global (packed stack entries when indices fit 24 bits; the timed
+// global instance's schedule and waves per SIMD chosen at upload), and with
 // or without the texture-sampling branch (TEX, only when a material samples).
 template <bool TEX>
 int LaunchMode(srt_context* c, const srt::KParams& kc, size_t lds, bool count, bool ldsm, bool pack) {
@@ -388,6 +391,8 @@ int LaunchMode(srt_context* c, const srt::KParams& kc, size_t lds, bool count, b
   if (count) return pack ? LaunchSamples<true, false, true, 256, TEX>(c, kc, lds)
                          : LaunchSamples<true, false, false, 256, TEX>(c, kc, lds);
   if (ldsm) return LaunchSamples<false, true, true, 1024, TEX>(c, kc, lds);
+  if (c->fused && c->global_waves == 5) return pack ? LaunchSamples<false, false, true, 256, TEX, true, 5>(c, kc, lds)
+                                                   : LaunchSamples<false, false, false, 256, TEX, true, 5>(c, kc, lds);
   if (c->fused) return pack ? LaunchSamples<false, false, true, 256, TEX, true>(c, kc, lds)
                             : LaunchSamples<false, false, false, 256, TEX, true>(c, kc, lds);
   return pack ? LaunchSamples<false, false, true, 256, TEX>(c, kc, lds)
@@ -437,9 +442,10 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
     } else if (ldsm) {
       kp.stack_base_f4 = kp.nodes_lds_f4 + kp.tris_f4;
       lds = lds_mode_bytes;
-    } else {  // LDS rings of kShortStack entries per lane, backed by HBM stacks (LaunchSamples)
+    } else {  // LDS rings of global_ring(waves) entries per lane, backed by HBM stacks (LaunchSamples)
       kp.stack_base_f4 = 0;
-      lds = (size_t)block * (c->lds_ok ? 2 : 3) * sizeof(uint32_t) * (size_t)srt::kShortStack;
+      const int gw = (!count && c->fused) ? c->global_waves : 4;  // LaunchMode's instance
+      lds = (size_t)block * (c->lds_ok ? 2 : 3) * sizeof(uint32_t) * (size_t)srt::global_ring(gw);
     }
     {  // light and material records in LDS behind the rest, when they fit (shading reads them there)
       lds = (lds + 15) & ~(size_t)15;
@@ -839,6 +845,8 @@ int srt_get_int(srt_context* c, const char* name, int* v) {
   else if (n == "bvh_count") *v = (int)c->bvh_count;
   else if (n == "resetAccumBuffer") *v = c->reset;
   else if (n == "showModel") *v = c->show_model;
+  else if (n == "scene.fused") *v = c->fused ? 1 : 0;
+  else if (n == "scene.global_waves") *v = c->global_waves;
   else return SRT_ERR_NOT_FOUND;
   return SRT_OK;
 }
@@ -994,6 +1002,12 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   // at 600 MB; SRT_GLOBAL_FUSED_MODE=1/0 forces either.
   const char* fu_env = std::getenv("SRT_GLOBAL_FUSED_MODE");
   c->fused = fu_env ? fu_env[0] == '1' : scene_mb < 600.0;
+  // Waves per SIMD of the fused instance: 5 (8-entry rings, some spills) while the tree is small
+  // enough that the extra rays in flight pay (torus knot 262 k, 20 MB: 5,405 -> 5,650 Mrays/s; Rubik
+  // forced global +6%; 100 k +2%; 300 k, 30 MB: +1%), else 4 (1 M, 101 MB: -7% with 5; 3 M: -7%).
+  // Crossover taken at 48 MB; SRT_GLOBAL_WAVES_MODE=4/5 forces either.
+  const char* gw_env = std::getenv("SRT_GLOBAL_WAVES_MODE");
+  c->global_waves = gw_env ? (gw_env[0] == '5' ? 5 : 4) : (scene_mb < 48.0 ? 5 : 4);
   bool laid = !(lay_env && lay_env[0] == '0') && LayoutNodes(nodes, n_nodes, bvhs, n_bvhs, align, &remap, &n_slots);
   if (!laid) {
     remap.resize(n_nodes);

@@ -454,7 +454,7 @@ __device__ __forceinline__ void trav_leaf(const KParams& kp, Counters& c, Trav& 
 // Internal sub-step: test both children's boxes; push c0 when both pass, go to
 // c1 if it passes, else to c0 if it passes.
 // (l0, h0, l1, h1): the child pair; (m0, g0, m1, g1): c1's child pair when `spine`.
-template <bool COUNT, bool LDSM, bool PACK>
+template <bool COUNT, bool LDSM, bool PACK, int RING = kShortStack>
 __device__ __forceinline__ void trav_internal_x(const KParams& kp, const Lane& ln, Counters& c, Trav& t,
                                                 const float4 l0, const float4 h0, const float4 l1, const float4 h1,
                                                 const float4 m0, const float4 g0, const float4 m1, const float4 g1,
@@ -470,14 +470,14 @@ __device__ __forceinline__ void trav_internal_x(const KParams& kp, const Lane& l
     if constexpr (LDSM) {
       slot_write<true>(ln.stk, ln.stride, t.sp, r_, n_, b_);
     } else {
-      if (t.sp - t.lo == kShortStack) {  // ring full: its oldest entry moves to HBM (rare)
+      if (t.sp - t.lo == RING) {  // ring full: its oldest entry moves to HBM (rare)
         uint32_t r, n;
         float bt;
-        slot_read<PACK>(ln.stk, ln.stride, t.lo & (kShortStack - 1), r, n, bt);
+        slot_read<PACK>(ln.stk, ln.stride, t.lo & (RING - 1), r, n, bt);
         slot_write<PACK>(ln.gstk, ln.gstride, t.lo, r, n, bt);
         ++t.lo;
       }
-      slot_write<PACK>(ln.stk, ln.stride, t.sp & (kShortStack - 1), r_, n_, b_);
+      slot_write<PACK>(ln.stk, ln.stride, t.sp & (RING - 1), r_, n_, b_);
     }
   };
   push_entry(r0, n0, b0);
@@ -508,7 +508,7 @@ __device__ __forceinline__ void trav_internal_x(const KParams& kp, const Lane& l
     }
   }
 }
-template <bool COUNT, bool LDSM, bool PACK>
+template <bool COUNT, bool LDSM, bool PACK, int RING = kShortStack>
 __device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln, Counters& c, Trav& t) {
   const uint32_t ref0 = t.ref | kp.ref_or;  // the child pair's first slot
   const bool spine = kSpine<LDSM> && (ref0 != t.ref);  // c1 is internal and its pair follows
@@ -522,10 +522,10 @@ __device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln,
     m1 = node4<LDSM>(kp, pi + 6);
     g1 = node4<LDSM>(kp, pi + 7);
   }
-  trav_internal_x<COUNT, LDSM, PACK>(kp, ln, c, t, l0, h0, l1, h1, m0, g0, m1, g1, spine);
+  trav_internal_x<COUNT, LDSM, PACK, RING>(kp, ln, c, t, l0, h0, l1, h1, m0, g0, m1, g1, spine);
 }
 
-template <bool LDSM, bool PACK>
+template <bool LDSM, bool PACK, int RING = kShortStack>
 __device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav& t);
 
 // Global-scene mode: one sub-step for both node kinds.  Lanes at an internal
@@ -534,7 +534,7 @@ __device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav
 // for both; then each kind's tests run on their lanes.  The memory-latency-bound
 // global mode trades the second kind's idle lanes for half the round trips;
 // each lane's steps, and so its decisions, are unchanged.
-template <bool COUNT, bool PACK>
+template <bool COUNT, bool PACK, int RING = kShortStack>
 __device__ __forceinline__ void trav_fused(const KParams& kp, const Lane& ln, Counters& c, Trav& t, bool any) {
   const bool at_int = t.cnt == 0u, at_leaf = trav_at_leaf(t.cnt);
   if (at_int | at_leaf) {
@@ -557,10 +557,11 @@ __device__ __forceinline__ void trav_fused(const KParams& kp, const Lane& ln, Co
       x[6] = p[6];
       x[7] = p[7];
     }
-    if (at_int) trav_internal_x<COUNT, false, PACK>(kp, ln, c, t, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], spine);
+    if (at_int)
+      trav_internal_x<COUNT, false, PACK, RING>(kp, ln, c, t, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], spine);
     else trav_leaf_x<COUNT, false>(kp, c, t, any, x);
   }
-  trav_pop<false, PACK>(kp, ln, t);
+  trav_pop<false, PACK, RING>(kp, ln, t);
 }
 
 // Nothing current: pop one entry (visited if it still beats the running
@@ -570,7 +571,7 @@ __device__ __forceinline__ void trav_fused(const KParams& kp, const Lane& ln, Co
 // emptied its stack, and `start` is never set during the sub-steps
 // (trav_finish sets it at the end of an iteration, trav_step clears it before
 // the first sub-step).
-template <bool LDSM, bool PACK>
+template <bool LDSM, bool PACK, int RING>
 __device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav& t) {
   if ((t.cnt == kNoneCnt) & (t.sp > 0)) {
     --t.sp;
@@ -582,7 +583,7 @@ __device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav
       slot_read<PACK>(ln.gstk, ln.gstride, t.sp, r, n, et);
       t.lo = t.sp;
     } else {
-      slot_read<PACK>(ln.stk, ln.stride, t.sp & (kShortStack - 1), r, n, et);
+      slot_read<PACK>(ln.stk, ln.stride, t.sp & (RING - 1), r, n, et);
     }
     const bool take = et < t.dist;
     t.ref = r;
@@ -604,25 +605,25 @@ __device__ __forceinline__ void trav_finish(const KParams& kp, Trav& t, bool any
   }
 }
 
-template <bool COUNT, bool LDSM, bool PACK, bool FUSE, int K>
+template <bool COUNT, bool LDSM, bool PACK, bool FUSE, int K, int RING = kShortStack>
 __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln, Counters& c, Trav& t, bool any) {
   if constexpr (FUSE) {
     static_assert(!LDSM, "fused sub-steps are a global-scene mode schedule");
     if constexpr (K < kFusedSteps) {
-      trav_fused<COUNT, PACK>(kp, ln, c, t, any);
-      trav_substeps<COUNT, LDSM, PACK, FUSE, K + 1>(kp, ln, c, t, any);
+      trav_fused<COUNT, PACK, RING>(kp, ln, c, t, any);
+      trav_substeps<COUNT, LDSM, PACK, FUSE, K + 1, RING>(kp, ln, c, t, any);
     }
   } else if constexpr (step_kind<LDSM>(K) != 0) {
     if constexpr (step_kind<LDSM>(K) == 'I') {
       DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K, t.cnt == 0);
-      if (t.cnt == 0) trav_internal<COUNT, LDSM, PACK>(kp, ln, c, t);
+      if (t.cnt == 0) trav_internal<COUNT, LDSM, PACK, RING>(kp, ln, c, t);
     } else {
       DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K, trav_at_leaf(t.cnt));
       if (trav_at_leaf(t.cnt)) trav_leaf<COUNT, LDSM>(kp, c, t, any);
     }
     DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K + 2, t.active & (t.cnt == kNoneCnt));
-    trav_pop<LDSM, PACK>(kp, ln, t);
-    trav_substeps<COUNT, LDSM, PACK, FUSE, K + 1>(kp, ln, c, t, any);
+    trav_pop<LDSM, PACK, RING>(kp, ln, t);
+    trav_substeps<COUNT, LDSM, PACK, FUSE, K + 1, RING>(kp, ln, c, t, any);
   }
 }
 
@@ -631,11 +632,13 @@ __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln,
 // node is of its kind, so a lane makes up to strlen(pattern) steps of
 // its own sequence per iteration, in order.  `any` selects the shadow-ray
 // (first hit) variant.
-template <bool COUNT, bool LDSM, bool PACK, bool FUSE>
+// RING: global-scene mode's LDS ring entries per lane (a power of two).
+template <bool COUNT, bool LDSM, bool PACK, bool FUSE, int RING = kShortStack>
 __device__ __forceinline__ void trav_step(const KParams& kp, const Lane& ln, Counters& c, Trav& t, f3 ro, f3 rd,
                                           bool any) {
+  static_assert((RING & (RING - 1)) == 0, "the LDS ring holds a power-of-two number of entries");
   if (t.start) trav_begin_bvh<COUNT, LDSM>(kp, c, t, ro, rd);  // only for BVHs after the first
-  trav_substeps<COUNT, LDSM, PACK, FUSE, 0>(kp, ln, c, t, any);
+  trav_substeps<COUNT, LDSM, PACK, FUSE, 0, RING>(kp, ln, c, t, any);
   trav_finish(kp, t, any);
 }
 

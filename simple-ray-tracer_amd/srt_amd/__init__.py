@@ -417,6 +417,12 @@ class Compute:
         elif name == "Height":
             self.height = int(val)
 
+    def GetInt(self, name: str) -> int:
+        """An int / uint / bool uniform's value, or "scene.fused" / "scene.global_waves" (srt_get_int)."""
+        v = C.c_int()
+        check(lib().srt_get_int(self.ctx, name.encode(), C.byref(v)), f"GetInt({name})")
+        return v.value
+
     def SetUInt(self, name: str, val: int):
         rc = lib().srt_set_uint(self.ctx, name.encode(), int(val) & 0xFFFFFFFF)
         if rc != _lib.SRT_ERR_NOT_FOUND:

@@ -185,6 +185,15 @@ def lib() -> C.CDLL:
     if _lib is None:
         if not LIB_PATH.exists():
             raise ImportError(f"{LIB_PATH} not built: run `make -C {PKG_DIR}` (or __graft_entry__.build())")
+        # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7 / libhsa-runtime64.so.1
+        # (same sonames as /opt/rocm's), so whichever is loaded first serves both.  Loading ours
+        # first and torch's CUDA later left torch on a runtime it was not built against, and the
+        # process aborted at exit ("free(): invalid pointer") after a test had used torch.cuda
+        # buffers; with torch loaded first, as bench.py does, both run on torch's runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         handle = C.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | C.RTLD_GLOBAL)
         for name, (res, args) in _SIGS.items():
             fn = getattr(handle, name)

@@ -8,6 +8,7 @@ one GPU per rank.
 """
 import os
 import pathlib
+import signal
 import socket
 import subprocess
 import sys
@@ -43,7 +44,7 @@ def _reference_frame():
 def _run_bench(tmp_path: pathlib.Path, world: int, band: int):
     port = _free_port()
     dump = tmp_path / f"frame_w{world}_b{band}.npz"
-    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
+    cmd = [sys.executable, "-X", "faulthandler", str(ROOT / "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
            "--width", str(W), "--height", str(H), "--spp", str(SPP), "--band-rows", str(band),
            "--no-cpu-baseline", "--no-global-leg", "--no-surface-leg", "--backend", "gloo", "--same-device", "--dump", str(dump)]
     procs = []
@@ -54,11 +55,18 @@ def _run_bench(tmp_path: pathlib.Path, world: int, band: int):
     outs = []
     for p in procs:
         try:
-            o, e = p.communicate(timeout=240)
-        except subprocess.TimeoutExpired:
+            o, e = p.communicate(timeout=120)
+        except subprocess.TimeoutExpired:  # every rank's Python stacks (faulthandler), then the failure
             for q in procs:
-                q.kill()
-            raise
+                q.send_signal(signal.SIGABRT)
+            tails = []
+            for q in procs:
+                try:
+                    tails.append(q.communicate(timeout=20)[1][-4000:])
+                except subprocess.TimeoutExpired:
+                    q.kill()
+                    tails.append("(no exit after SIGABRT)")
+            raise AssertionError("ranks did not finish in 120 s:\n" + "\n----\n".join(tails))
         outs.append((p.returncode, o, e))
     for rc, o, e in outs:
         assert rc == 0, e[-3000:]

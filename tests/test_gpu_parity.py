@@ -25,7 +25,11 @@ def rubik():
     return S.load_obj(OBJECTS / "Rubik" / "Rubik.obj")
 
 
-def gpu_render(setup, spp, *, per_frame=False, **kw):
+def gpu_render(setup, spp, *, per_frame=False, timed=True, **kw):
+    """The frame through the counting instance of sample_kernel (fused launch, with CheckHit counts) or
+    per-frame dispatches; with `timed`, the fused launch is rendered again through the timed instance the
+    benchmark measures (in global-scene mode another schedule: fused sub-steps, more waves per SIMD), which
+    must give the same frame bit for bit."""
     r = R.Renderer(setup, **kw)
     try:
         if per_frame:
@@ -35,7 +39,14 @@ def gpu_render(setup, spp, *, per_frame=False, **kw):
         else:
             r.render(spp, count=True)
         r.finish()
-        return r.accum(), r.output(), r.compute.stats()
+        acc, out, st = r.accum(), r.output(), r.compute.stats()
+        if timed and not per_frame:
+            r.render(spp)
+            r.finish()
+            eq = bits_equal(r.accum(), acc)
+            assert eq.all(), f"timed instance: {(~eq).sum()} accumulation values differ from the counting instance"
+            assert (r.output() == out).all()
+        return acc, out, st
     finally:
         r.close()
 
@@ -198,13 +209,16 @@ def test_surface_mesh_global_mode():
 @pytest.mark.parametrize("env", [{"SRT_NODE_ALIGN": "1"}, {"SRT_NODE_LAYOUT": "0"},
                                  {"SRT_NODE_ALIGN": "1", "SRT_GLOBAL_FUSED_MODE": "1"},
                                  {"SRT_NODE_ALIGN": "0", "SRT_GLOBAL_FUSED_MODE": "0"},
-                                 {"SRT_NODE_LAYOUT": "0", "SRT_GLOBAL_FUSED_MODE": "1"}])
+                                 {"SRT_NODE_LAYOUT": "0", "SRT_GLOBAL_FUSED_MODE": "1"},
+                                 {"SRT_GLOBAL_WAVES_MODE": "4"},
+                                 {"SRT_NODE_ALIGN": "1", "SRT_GLOBAL_WAVES_MODE": "5"}])
 def test_node_layouts_global_mode(monkeypatch, env):
     """The device node layouts (pathtrace.hip LayoutNodes): line-aligned right-child chains (chosen for
     scenes past the Infinity Cache) and the reference's own order (no right-spine double steps) render
     the oracle's frame in global-scene mode, two models with a moved second one included; so do both
     traversal schedules (fused sub-steps, chosen with the dense layout, and the IL pattern) on
-    every layout."""
+    every layout, and the fused schedule's timed instance at 4 and 5 waves per SIMD (8-entry LDS
+    rings: deeper stacks spill to HBM more often)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     setup = R.make_setup(48, 40, show_model=True, models=[R.synthetic_model(30000, seed=3)])
@@ -215,6 +229,32 @@ def test_node_layouts_global_mode(monkeypatch, env):
     frame[3, :3] = (1.5, -2.0, 0.5)
     two.scene.bvhs[1]["frame"] = frame.reshape(16)
     assert_parity(two, 2)
+
+
+def test_global_schedule_chosen_by_scene_size():
+    """srt_upload_scene's choices for the timed global-scene instance, as bench.py reports them: the torus
+    knot (20 MB of nodes + triangles) takes fused sub-steps at 5 waves per SIMD, a 1 M soup (101 MB)
+    fused sub-steps at 4; the environment forces either."""
+    def chosen(model, env=None):
+        old = {k: os.environ.get(k) for k in (env or {})}
+        os.environ.update(env or {})
+        try:
+            r = R.Renderer(R.make_setup(16, 8, show_model=True, models=[model]))
+            try:
+                return r.compute.GetInt("scene.fused"), r.compute.GetInt("scene.global_waves")
+            finally:
+                r.close()
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k)
+                else:
+                    os.environ[k] = v
+
+    knot = R.torus_knot_model()
+    assert chosen(knot) == (1, 5)
+    assert chosen(knot, {"SRT_GLOBAL_WAVES_MODE": "4"}) == (1, 4)
+    assert chosen(R.synthetic_model(1_000_000, seed=1)) == (1, 4)
 
 
 @pytest.mark.parametrize("force_global", ["1", "0"])

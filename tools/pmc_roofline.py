@@ -25,14 +25,14 @@ only = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv el
 root = pathlib.Path(__file__).resolve().parent.parent
 
 LEGS = {  # kernel instance -> the workloads bench.py runs on it, in launch order (one timed launch each)
-    "void srt::sample_kernel<false, true, true, 1024, false, false>": ["rubik_1920x1080_256spp"],
-    "void srt::sample_kernel<false, false, true, 256, false, true>": ["synthetic1000000_1920x1080_16spp",
-                                                                "torusknot262144_1920x1080_64spp"],
+    "void srt::sample_kernel<false, true, true, 1024, false, false, 4>": ["rubik_1920x1080_256spp"],
+    "void srt::sample_kernel<false, false, true, 256, false, true, 4>": ["synthetic1000000_1920x1080_16spp"],
+    "void srt::sample_kernel<false, false, true, 256, false, true, 5>": ["torusknot262144_1920x1080_64spp"],
 }
 
 
-if only:
-    LEGS = {"void srt::sample_kernel<false, false, true, 256, false, " + ("false>" if "--il" in sys.argv else "true>"): [only]}
+if only:  # the one timed global-scene instance of the run, whatever its waves per SIMD
+    LEGS = {"void srt::sample_kernel<false, false, true, 256, false, " + ("false," if "--il" in sys.argv else "true,"): [only]}
 # --sum: a single-workload run whose timed step may be several launches (sample-buffer chunks, e.g. C4):
 # the counters of every non-counting sample_kernel dispatch are summed (bench's kernel_ms sums the same
 # launches' HIP-event times); the counting run is the <true, ...> instance and is left out.
