@@ -39,15 +39,16 @@ def assemble_host(gathered: np.ndarray, height: int, band_rows: int) -> np.ndarr
     return out
 
 
-def gather_bands(local, dst: int = 0):
+def gather_bands(local, dst: int = 0, collective: bool = False):
     """Gather every rank's equal-size band buffer to `dst` (one collective).  Returns the stacked
-    [nranks, ...] tensor on dst, None elsewhere."""
+    [nranks, ...] tensor on dst, None elsewhere.  One rank skips the collective unless `collective`
+    (the one-GPU test of the RCCL path)."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size()
     rank = dist.get_rank()
-    if world == 1:
+    if world == 1 and not collective:
         return local.unsqueeze(0)
     # gloo gathers host tensors: a device buffer is staged through the host and the stacked result
     # moved back (multi-rank tests on one GPU); RCCL ("nccl") gathers device memory directly over xGMI

@@ -87,3 +87,51 @@ def test_bench_ranks_assemble_the_one_rank_frame(tmp_path, world, band):
     assert (out == out1).all()
     j = json.loads(line)
     assert j["n_gpus"] == world and j["value"] > 0
+
+
+_RCCL_SCRIPT = r"""
+import sys, numpy as np, torch, torch.distributed as dist
+sys.path[:0] = sys.argv[2:]
+from srt_amd import parallel as PAR
+from srt_amd import render as R
+from conftest import OBJECTS
+dist.init_process_group("nccl", init_method="tcp://127.0.0.1:" + sys.argv[1], world_size=1, rank=0,
+                        device_id=torch.device("cuda", 0))
+W, H, SPP, BAND = 64, 40, 2, 2
+setup = R.make_setup(W, H, show_model=True, models=[R.rubik_model(OBJECTS)])
+r = R.Renderer(setup, rank=0, nranks=1, band_rows=BAND)
+rows_pad = PAR.rows_pad(H, BAND, 1)
+acc = torch.zeros((rows_pad, W, 4), dtype=torch.float32, device="cuda")
+out = torch.zeros((rows_pad, W), dtype=torch.int32, device="cuda")
+r.compute.set_image_buffers(acc.data_ptr(), out.data_ptr())
+r.render(SPP)
+r.finish()
+stacked = PAR.gather_bands(acc, dst=0, collective=True)   # dist.gather of device memory over RCCL
+full = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+full_out = torch.empty((H, W), dtype=torch.int32, device="cuda")
+r.compute.assemble_bands(stacked.data_ptr(), 1, rows_pad, BAND, SPP + 1, full.data_ptr(), full_out.data_ptr())
+r.finish()
+torch.cuda.synchronize()
+r.close()
+np.savez("rccl_frame.npz", accum=full.cpu().numpy(),
+         out=full_out.cpu().numpy().view(np.uint8).reshape(H, W, 4))
+print("OK", dist.get_backend())
+dist.destroy_process_group()
+"""
+
+
+def test_rccl_gather_through_torch_distributed(tmp_path):
+    """bench.py's exchange over the "nccl" backend (RCCL), which the gloo tests above stage through the
+    host: one rank, the collective forced, device memory gathered and assembled; the frame is the oracle's."""
+    from conftest import PKG, oracle_render
+
+    script = tmp_path / "rccl_one.py"
+    script.write_text(_RCCL_SCRIPT)
+    res = subprocess.run([sys.executable, str(script), str(_free_port()), str(PKG), str(ROOT / "tests"), str(ROOT)],
+                         capture_output=True, text=True, timeout=120, cwd=tmp_path)
+    last = res.stdout.strip().splitlines()[-1] if res.stdout.strip() else ""
+    assert res.returncode == 0 and last == "OK nccl", res.stdout[-2000:] + res.stderr[-3000:]
+    with np.load(tmp_path / "rccl_frame.npz") as z:
+        acc, out = z["accum"], z["out"]
+    want = oracle_render(R.make_setup(64, 40, show_model=True, models=[R.rubik_model(OBJECTS)]), 2)
+    assert bits_equal(acc, want[0]).all() and (out == want[1]).all()
