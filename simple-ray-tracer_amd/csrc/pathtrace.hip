@@ -132,13 +132,14 @@ struct srt_context {
   int tail_claims = 16;  // SRT_TAIL_CLAIMS: claims per wave before the end from which claims take one batch
   int trav_frac16 = 9;                 // SRT_TRAV_FRAC16 (measured best on Rubik 1080p with the 16-sub-step pattern)
   int bounce_cap = 1 << 20;            // SRT_BOUNCE_CAP: bounces after which a path is cut (counted)
-  int trav_frac16_global = 9;
+  int trav_frac16_global = 9;          // SRT_TRAV_FRAC16_GLOBAL: the same threshold for global-scene mode
+  bool trav_frac16_global_env = false; // (set: every global instance uses it; else the fused 4-wave one takes 7)
   bool pool_launched = false;          // the last render ran pool_kernel (srt_finish checks its watchdog)
   int pool = 0;                        // SRT_POOL=1: LDS mode runs pool_kernel (workgroup ray pools)
   int pool_batch = 64;                 // SRT_POOL_BATCH: queued hits a shading wave waits for
   int pool_tlow = 32;                  // SRT_POOL_TLOW: trace + spare records under which shading waves take fewer
   int pool_slots_max = 4096;           // SRT_POOL_SLOTS: at most this many records
-  int pool_deadline_ms = 30000;        // SRT_POOL_DEADLINE_MS: pool_kernel's watchdog          // SRT_TRAV_FRAC16_GLOBAL: the same threshold for global-scene mode
+  int pool_deadline_ms = 30000;        // SRT_POOL_DEADLINE_MS: pool_kernel's watchdog
   int num_cus = 256;
   // stats
   unsigned long long* d_stats = nullptr;
@@ -368,11 +369,16 @@ int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
   }
 #endif
   {  // single-batch claims for the last tail_claims * kClaim batches per wave (sample_kernel; measured
-     // with tools/tail_sweep.sh: 2 -> 16 halves the launch's tail)
+     // in round 1: 2 -> 16 halves the launch's tail)
     const long long waves = (long long)blocks * (BLOCK / 64);
     const long long n_batches = (long long)((kp.W + 7) >> 3) * ((kp.local_rows + 7) >> 3) * kp.nframes;
     kp.tail_start = (int)std::max<long long>(0, n_batches - (long long)c->tail_claims * srt::kClaim * waves);
   }
+  // the early-break threshold of the fused 4-wave instance (trees of 48-600 MB): 7, where the
+  // latency-bound soups gain (1 M: 1,370 -> 1,413-1,418 Mrays/s; 3 M: 939 -> 971) and the 5-wave
+  // (torus knot) and IL (C5) instances lose
+  if constexpr (!LDSM && FUSE && GW == 4)
+    if (!c->trav_frac16_global_env) kp.trav_frac16 = 7;
   HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
   hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX, FUSE, GW>), dim3(blocks), dim3(BLOCK), lds, c->stream,
                      kp);
@@ -723,7 +729,7 @@ int srt_create(int device, void* stream, srt_context** out) {
   if (const char* e = std::getenv("SRT_TILE_ORDER")) c->tile_schedule = e[0] != '0';
   if (const char* e = std::getenv("SRT_TRAV_FRAC16")) c->trav_frac16 = std::max(0, std::min(16, std::atoi(e)));
   if (const char* e = std::getenv("SRT_TRAV_FRAC16_GLOBAL"))
-    c->trav_frac16_global = std::max(0, std::min(16, std::atoi(e)));
+    c->trav_frac16_global = std::max(0, std::min(16, std::atoi(e))), c->trav_frac16_global_env = true;
   {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
