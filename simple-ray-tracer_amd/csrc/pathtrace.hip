@@ -37,6 +37,7 @@
 
 #include "kernels.hpp"
 #include "pool.hpp"
+#include "wavefront.hpp"
 
 // ===========================================================================
 // host side: the device context behind the C ABI
@@ -141,6 +142,29 @@ struct srt_context {
   int pool_slots_max = 4096;           // SRT_POOL_SLOTS: at most this many records
   int pool_deadline_ms = 30000;        // SRT_POOL_DEADLINE_MS: pool_kernel's watchdog
   int num_cus = 256;
+  // wavefront mode (wavefront.hpp): global-scene launches through wf_logic / wf_shade / wf_trace
+  int wavefront = -1;                  // SRT_WAVEFRONT=1/0 forces it on / off; -1: by scene (wf_scene)
+  bool wf_scene = false;               // chosen at upload
+  uint32_t wf_slots = 1u << 21;        // SRT_WF_SLOTS: path slots in HBM
+  int wf_waves = 6;                    // SRT_WF_WAVES: waves per SIMD of wf_trace_kernel (4, 5, 6 or 8)
+  float4* d_wf_rec = nullptr;
+  uint2* d_wf_res = nullptr;
+  uint32_t *d_wf_state = nullptr, *d_wf_rayq = nullptr, *d_wf_hitq = nullptr, *d_wf_ctl = nullptr,
+           *d_wf_items = nullptr;
+  uint32_t wf_cap = 0;
+  uint32_t* h_wf_poll = nullptr;       // pinned: (live, items) of two polled iterations
+  bool wf_launched = false;            // the last render went through wavefront mode
+  // treelet scheduling of wavefront mode's trace stage (wavefront.hpp wf_top_kernel / wf_bottom_kernel)
+  int treelets = -1;                   // SRT_TREELETS=1/0 forces it on / off; -1: by scene (tl_scene)
+  bool tl_scene = false;               // chosen at upload
+  int treelet_depth = 0;               // SRT_TREELET_DEPTH: depth of the treelet roots (0: by scene size)
+  uint32_t n_treelets = 0;             // of the uploaded scene (0: no flagged copy)
+  float4* d_nodes_t = nullptr;         // the node array with treelet roots flagged
+  uint32_t* d_troot = nullptr;         // per treelet: its root's child index
+  float4* d_tl_ray = nullptr;
+  uint32_t *d_tl_stk = nullptr, *d_tl_slist = nullptr, *d_tl_skey = nullptr, *d_tl_blist = nullptr,
+           *d_tl_rlist = nullptr, *d_tl_count = nullptr, *d_tl_fill = nullptr;
+  uint32_t tl_cap = 0, tl_count_cap = 0;
   // stats
   unsigned long long* d_stats = nullptr;
   unsigned long long* d_nan = nullptr;  // NaN path samples since the last srt_reset_stats
@@ -419,6 +443,220 @@ int LaunchPool(srt_context* c, srt::KParams kp, size_t lds) {
   return SRT_OK;
 }
 
+// Wavefront mode (wavefront.hpp): the trace-stage kernels' instances (stack entry packing, fused
+// sub-steps or the IL pattern, waves per SIMD) and their grids: as many 256-lane blocks as are resident.
+template <typename F>
+int Resident(srt_context* c, F* fn, size_t lds, int* blocks) {
+  const void* key = reinterpret_cast<const void*>(fn);
+  int per_cu = 0;
+  for (const auto& e : c->occupancy)
+    if (e.fn == key && e.lds == lds) per_cu = e.per_cu;
+  if (per_cu == 0) {
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds));
+    per_cu = std::max(per_cu, 1);
+    c->occupancy.push_back({key, lds, per_cu});
+  }
+  *blocks = c->num_cus * per_cu;
+  return SRT_OK;
+}
+// The trace stage of one iteration: wf_trace_kernel, or with treelets (kp_top: the flagged node copy)
+// wf_top_kernel -> wf_scan_kernel -> wf_scatter_kernel -> wf_bottom_kernel.  With `launch` false it
+// only sizes the grids: *lanes = the most lanes any of them runs (their HBM stacks).
+template <bool PACK, bool FUSE, int GW>
+int WfStage(srt_context* c, const srt::KParams& kp, const srt::KParams& kp_top, const srt::WfParams& w, bool tl,
+            bool launch, size_t* lanes) {
+  const size_t ring_bytes = (size_t)256 * (PACK ? 2 : 3) * sizeof(uint32_t);
+  const size_t lds = ring_bytes * (size_t)srt::global_ring(GW);
+  int blocks = 0;
+  if (!tl) {
+    int rc = Resident(c, srt::wf_trace_kernel<PACK, FUSE, GW>, lds, &blocks);
+    if (rc) return rc;
+    if (lanes) *lanes = (size_t)blocks * 256;
+    if (launch) {
+      hipLaunchKernelGGL((srt::wf_trace_kernel<PACK, FUSE, GW>), dim3(blocks), dim3(256), lds, c->stream, kp, w);
+      HIP_OK(hipGetLastError());
+    }
+    return SRT_OK;
+  }
+  const size_t lds_top = ring_bytes * (size_t)srt::kShortStack;
+  int tblocks = 0;
+  int rc = Resident(c, srt::wf_top_kernel<PACK, FUSE>, lds_top, &tblocks);
+  if (rc) return rc;
+  rc = Resident(c, srt::wf_bottom_kernel<PACK, FUSE, GW>, lds, &blocks);
+  if (rc) return rc;
+  if (lanes) *lanes = (size_t)std::max(blocks, tblocks) * 256;
+  if (launch) {
+    hipLaunchKernelGGL((srt::wf_top_kernel<PACK, FUSE>), dim3(tblocks), dim3(256), lds_top, c->stream, kp_top, w);
+    hipLaunchKernelGGL(srt::wf_scan_kernel, dim3(1), dim3(1024), 0, c->stream, w);
+    hipLaunchKernelGGL(srt::wf_scatter_kernel, dim3((w.slots + 255) / 256), dim3(256), 0, c->stream, w);
+    hipLaunchKernelGGL((srt::wf_bottom_kernel<PACK, FUSE, GW>), dim3(blocks), dim3(256), lds, c->stream, kp, w);
+    HIP_OK(hipGetLastError());
+  }
+  return SRT_OK;
+}
+template <bool PACK, bool FUSE>
+int WfStageWaves(srt_context* c, const srt::KParams& kp, const srt::KParams& kt, const srt::WfParams& w, bool tl,
+                 bool launch, size_t* lanes) {
+  switch (c->wf_waves) {
+    case 4: return WfStage<PACK, FUSE, 4>(c, kp, kt, w, tl, launch, lanes);
+    case 5: return WfStage<PACK, FUSE, 5>(c, kp, kt, w, tl, launch, lanes);
+    case 8: return WfStage<PACK, FUSE, 8>(c, kp, kt, w, tl, launch, lanes);
+    default: return WfStage<PACK, FUSE, 6>(c, kp, kt, w, tl, launch, lanes);
+  }
+}
+int WfTrace(srt_context* c, const srt::KParams& kp, const srt::KParams& kt, const srt::WfParams& w, bool tl,
+            bool launch, size_t* lanes) {
+  const bool pack = c->lds_ok;
+  if (c->fused) return pack ? WfStageWaves<true, true>(c, kp, kt, w, tl, launch, lanes)
+                            : WfStageWaves<false, true>(c, kp, kt, w, tl, launch, lanes);
+  return pack ? WfStageWaves<true, false>(c, kp, kt, w, tl, launch, lanes)
+              : WfStageWaves<false, false>(c, kp, kt, w, tl, launch, lanes);
+}
+
+// One chunk of frames through the wavefront kernels: iterations of logic -> shade -> trace over
+// c->wf_slots path slots until every sample item is taken and no slot is live.  The host polls the
+// live count of every 8th iteration one group late (a pinned copy and an event), so the stream stays
+// full; the few iterations issued past the end find empty queues and return at once.
+int LaunchWavefront(srt_context* c, srt::KParams kp, bool tex) {
+  constexpr int kMaxIters = 1 << 16;
+  const uint32_t P = c->wf_slots;
+  if (P > c->wf_cap) {
+    FreeDev(c->d_wf_rec); FreeDev(c->d_wf_res); FreeDev(c->d_wf_state); FreeDev(c->d_wf_rayq); FreeDev(c->d_wf_hitq);
+    c->d_wf_rec = nullptr; c->d_wf_res = nullptr; c->d_wf_state = c->d_wf_rayq = c->d_wf_hitq = nullptr;
+    c->wf_cap = 0;
+    HIP_OK(hipMalloc(&c->d_wf_rec, sizeof(float4) * 7 * (size_t)P));
+    HIP_OK(hipMalloc(&c->d_wf_res, sizeof(uint2) * (size_t)P));
+    HIP_OK(hipMalloc(&c->d_wf_state, sizeof(uint32_t) * (size_t)P));
+    HIP_OK(hipMalloc(&c->d_wf_rayq, sizeof(uint32_t) * (size_t)P));
+    HIP_OK(hipMalloc(&c->d_wf_hitq, sizeof(uint32_t) * (size_t)P));
+    c->wf_cap = P;
+  }
+  if (!c->d_wf_ctl) {
+    HIP_OK(hipMalloc(&c->d_wf_ctl, sizeof(uint32_t) * srt::WQ_WORDS * (size_t)kMaxIters));
+    HIP_OK(hipMalloc(&c->d_wf_items, sizeof(uint32_t)));
+    HIP_OK(hipHostMalloc(&c->h_wf_poll, 4 * sizeof(uint32_t), hipHostMallocDefault));
+  }
+  const long long n_items = 64LL * ((kp.W + 7) >> 3) * ((kp.local_rows + 7) >> 3) * kp.nframes;
+  if (n_items >= (1LL << 31)) {  // Launch bounds the frames per chunk so this cannot happen
+    srt::SetError("wavefront mode: more than 2^31 sample items in one chunk");
+    return SRT_ERR_LIMIT;
+  }
+  HIP_OK(hipMemsetAsync(c->d_wf_state, 0, sizeof(uint32_t) * (size_t)P, c->stream));
+  HIP_OK(hipMemsetAsync(c->d_wf_items, 0, sizeof(uint32_t), c->stream));
+  HIP_OK(hipMemsetAsync(c->d_wf_ctl, 0, sizeof(uint32_t) * srt::WQ_WORDS * (size_t)kMaxIters, c->stream));
+  srt::WfParams w;
+  w.rec = c->d_wf_rec;
+  w.res = c->d_wf_res;
+  w.state = c->d_wf_state;
+  w.rayq = c->d_wf_rayq;
+  w.hitq = c->d_wf_hitq;
+  w.ctl = c->d_wf_ctl;
+  w.items = c->d_wf_items;
+  w.slots = P;
+  w.n_items = (uint32_t)n_items;
+  w.iter = 0;
+  kp.lights_lds = 0;  // the wavefront kernels keep no LDS copies of lights / materials
+  kp.mats_lds = 0;
+  const bool tl = c->n_treelets > 0 && (c->treelets >= 0 ? c->treelets == 1 : c->tl_scene);
+  if (tl) {
+    if (P > c->tl_cap) {
+      FreeDev(c->d_tl_ray); FreeDev(c->d_tl_stk); FreeDev(c->d_tl_slist); FreeDev(c->d_tl_skey);
+      FreeDev(c->d_tl_blist); FreeDev(c->d_tl_rlist);
+      c->d_tl_ray = nullptr;
+      c->d_tl_stk = c->d_tl_slist = c->d_tl_skey = c->d_tl_blist = c->d_tl_rlist = nullptr;
+      c->tl_cap = 0;
+      HIP_OK(hipMalloc(&c->d_tl_ray, sizeof(float4) * 4 * (size_t)P));
+      HIP_OK(hipMalloc(&c->d_tl_stk, sizeof(uint32_t) * 3 * srt::kTopStack * (size_t)P));
+      HIP_OK(hipMalloc(&c->d_tl_slist, sizeof(uint32_t) * (size_t)P));
+      HIP_OK(hipMalloc(&c->d_tl_skey, sizeof(uint32_t) * (size_t)P));
+      HIP_OK(hipMalloc(&c->d_tl_blist, sizeof(uint32_t) * (size_t)P));
+      HIP_OK(hipMalloc(&c->d_tl_rlist, sizeof(uint32_t) * 2 * (size_t)P));
+      c->tl_cap = P;
+    }
+    if (c->n_treelets > c->tl_count_cap) {
+      FreeDev(c->d_tl_count); FreeDev(c->d_tl_fill);
+      c->d_tl_count = c->d_tl_fill = nullptr;
+      c->tl_count_cap = 0;
+      HIP_OK(hipMalloc(&c->d_tl_count, sizeof(uint32_t) * (size_t)c->n_treelets));
+      HIP_OK(hipMalloc(&c->d_tl_fill, sizeof(uint32_t) * (size_t)c->n_treelets));
+      c->tl_count_cap = c->n_treelets;
+    }
+    HIP_OK(hipMemsetAsync(c->d_tl_count, 0, sizeof(uint32_t) * (size_t)c->n_treelets, c->stream));
+    w.tray = c->d_tl_ray;
+    w.tstk = c->d_tl_stk;
+    w.slist = c->d_tl_slist;
+    w.skey = c->d_tl_skey;
+    w.blist = c->d_tl_blist;
+    w.rlist[0] = c->d_tl_rlist;
+    w.rlist[1] = c->d_tl_rlist + P;
+    w.tcount = c->d_tl_count;
+    w.tfill = c->d_tl_fill;
+    w.troot = c->d_troot;
+    w.n_treelets = c->n_treelets;
+  } else {
+    w.tray = nullptr;
+    w.tstk = w.slist = w.skey = w.blist = w.rlist[0] = w.rlist[1] = w.tcount = w.tfill = nullptr;
+    w.troot = nullptr;
+    w.n_treelets = 0;
+  }
+  srt::KParams kt = kp;  // the top kernel walks the flagged node copy
+  if (tl) kt.nodes = c->d_nodes_t;
+  size_t lanes = 0;
+  int rc = WfTrace(c, kp, kt, w, tl, false, &lanes);
+  if (rc) return rc;
+  {  // every trace lane's full stack in HBM, behind its LDS ring
+    const size_t need = lanes * (c->lds_ok ? 2 : 3) * sizeof(uint32_t) * (size_t)kp.stack_entries;
+    if (need > c->gstack_bytes) {
+      FreeDev(c->d_gstack);
+      c->d_gstack = nullptr;
+      c->gstack_bytes = 0;
+      HIP_OK(hipMalloc(&c->d_gstack, need));
+      c->gstack_bytes = need;
+    }
+    kp.gstack = kt.gstack = c->d_gstack;
+    kp.gstack_stride = kt.gstack_stride = (int)lanes;
+  }
+  const dim3 sgrid((P + 255) / 256);
+  hipEvent_t poll_ev[2];
+  HIP_OK(hipEventCreateWithFlags(&poll_ev[0], hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&poll_ev[1], hipEventDisableTiming));
+  HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
+  int it = 0;
+  bool done = false;
+  for (; it < kMaxIters && !done; ++it) {
+    w.iter = it;
+    hipLaunchKernelGGL(srt::wf_logic_kernel, sgrid, dim3(256), 0, c->stream, kp, w);
+    if (tex) hipLaunchKernelGGL(srt::wf_shade_kernel<true>, sgrid, dim3(256), 0, c->stream, kp, w);
+    else hipLaunchKernelGGL(srt::wf_shade_kernel<false>, sgrid, dim3(256), 0, c->stream, kp, w);
+    HIP_OK(hipGetLastError());
+    rc = WfTrace(c, kp, kt, w, tl, true, nullptr);
+    if (rc) break;
+    if ((it & 7) == 7) {
+      const int g = (it >> 3) & 1;
+      HIP_OK(hipMemcpyAsync(c->h_wf_poll + 2 * g, c->d_wf_ctl + (size_t)srt::WQ_WORDS * it + srt::WQ_LIVE,
+                            sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+      HIP_OK(hipMemcpyAsync(c->h_wf_poll + 2 * g + 1, c->d_wf_items, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                            c->stream));
+      HIP_OK(hipEventRecord(poll_ev[g], c->stream));
+      if (it >= 15) {  // the previous group's poll
+        HIP_OK(hipEventSynchronize(poll_ev[g ^ 1]));
+        const uint32_t live = c->h_wf_poll[2 * (g ^ 1)], items = c->h_wf_poll[2 * (g ^ 1) + 1];
+        done = live == 0 && (long long)items >= n_items;
+      }
+    }
+  }
+  (void)hipEventDestroy(poll_ev[0]);
+  (void)hipEventDestroy(poll_ev[1]);
+  if (rc) return rc;
+  if (!done) {
+    srt::SetError("wavefront mode: iteration limit reached");
+    return SRT_ERR_LIMIT;
+  }
+  HIP_OK(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
+  c->wf_launched = true;
+  return SRT_OK;
+}
+
 // Runs frames kp.frame_first .. + kp.nframes - 1 (or the reset frame) through
 // sample_kernel + accumulate_kernel, in chunks that fit the sample buffer.
 int Launch(srt_context* c, srt::KParams& kp, bool count) {
@@ -502,7 +740,10 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   // frames per launch: what the sample buffer holds, and n_tiles * frames < 2^31 (the kernel's batch index)
   const size_t n_tiles = (size_t)((kp.W + 7) >> 3) * (size_t)((kp.local_rows + 7) >> 3);
   // (less 2^20: the batch counter overshoots the end by up to (kClaim + 1) claims per wave)
-  const size_t max_frames = std::max<size_t>(1, ((size_t)0x7FFFFFFF - ((size_t)1 << 20)) / std::max<size_t>(1, n_tiles));
+  // wavefront mode (global-scene, timed launches): its sample items (64 per batch) < 2^31 per chunk
+  const bool wf = !ldsm && !count && kp.show_model && (c->wavefront >= 0 ? c->wavefront == 1 : c->wf_scene);
+  const size_t max_frames = std::max<size_t>(
+      1, ((size_t)0x7FFFFFFF - ((size_t)1 << 20)) / std::max<size_t>(1, n_tiles) / (wf ? 64 : 1));
   const int chunk = (int)std::max<size_t>(
       1, std::min<size_t>(std::min<size_t>((size_t)kp.nframes, max_frames), c->lbuf_cap / per_frame));
   const size_t need = per_frame * (size_t)chunk;
@@ -567,6 +808,7 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
     // LDS mode: packed entries (lds_ok); global-scene mode: packed when indices fit 24 bits
     const bool pack = c->lds_ok;
     if (pool) rc = count ? LaunchPool<true>(c, kc, lds) : LaunchPool<false>(c, kc, lds);
+    else if (wf) rc = LaunchWavefront(c, kc, c->sample_textures);
     else rc = c->sample_textures ? LaunchMode<true>(c, kc, lds, count, ldsm, pack)
                                  : LaunchMode<false>(c, kc, lds, count, ldsm, pack);
     if (rc) return rc;
@@ -725,6 +967,11 @@ int srt_create(int device, void* stream, srt_context** out) {
   if (const char* e = std::getenv("SRT_POOL_TLOW")) c->pool_tlow = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("SRT_POOL_SLOTS")) c->pool_slots_max = std::max(64, std::atoi(e));
   if (const char* e = std::getenv("SRT_POOL_DEADLINE_MS")) c->pool_deadline_ms = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("SRT_WAVEFRONT")) c->wavefront = e[0] == '1' ? 1 : 0;
+  if (const char* e = std::getenv("SRT_WF_SLOTS")) c->wf_slots = (uint32_t)std::max(256L, std::min(1L << 28, std::atol(e)));
+  if (const char* e = std::getenv("SRT_WF_WAVES")) c->wf_waves = std::atoi(e);
+  if (const char* e = std::getenv("SRT_TREELETS")) c->treelets = e[0] == '1' ? 1 : 0;
+  if (const char* e = std::getenv("SRT_TREELET_DEPTH")) c->treelet_depth = std::max(0, std::min(srt::kTopStack - 1, std::atoi(e)));
   if (const char* e = std::getenv("SRT_TAIL_CLAIMS")) c->tail_claims = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("SRT_TILE_ORDER")) c->tile_schedule = e[0] != '0';
   if (const char* e = std::getenv("SRT_TRAV_FRAC16")) c->trav_frac16 = std::max(0, std::min(16, std::atoi(e)));
@@ -768,6 +1015,11 @@ int srt_destroy(srt_context* c) {
   FreeDev(c->d_tex); FreeDev(c->d_tex_info); FreeDev(c->d_tri_uv);
   FreeDev(c->d_noise_xy); FreeDev(c->d_noise_u); FreeDev(c->d_stats); FreeDev(c->d_nan); FreeDev(c->d_lbuf); FreeDev(c->d_gstack);
   FreeDev(c->d_batch_ctr); FreeDev(c->d_tile_cost); FreeDev(c->d_tile_order);
+  FreeDev(c->d_wf_rec); FreeDev(c->d_wf_res); FreeDev(c->d_wf_state); FreeDev(c->d_wf_rayq); FreeDev(c->d_wf_hitq);
+  FreeDev(c->d_wf_ctl); FreeDev(c->d_wf_items);
+  FreeDev(c->d_nodes_t); FreeDev(c->d_troot); FreeDev(c->d_tl_ray); FreeDev(c->d_tl_stk); FreeDev(c->d_tl_slist);
+  FreeDev(c->d_tl_skey); FreeDev(c->d_tl_blist); FreeDev(c->d_tl_rlist); FreeDev(c->d_tl_count); FreeDev(c->d_tl_fill);
+  if (c->h_wf_poll) (void)hipHostFree(c->h_wf_poll);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (!c->images_external) { FreeDev(c->d_accum); FreeDev(c->d_out); }
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -853,6 +1105,9 @@ int srt_get_int(srt_context* c, const char* name, int* v) {
   else if (n == "showModel") *v = c->show_model;
   else if (n == "scene.fused") *v = c->fused ? 1 : 0;
   else if (n == "scene.global_waves") *v = c->global_waves;
+  else if (n == "scene.wavefront") *v = c->wavefront >= 0 ? c->wavefront : (c->wf_scene ? 1 : 0);
+  else if (n == "scene.wf_waves") *v = c->wf_waves;
+  else if (n == "scene.treelets") *v = (int)c->n_treelets;
   else return SRT_ERR_NOT_FOUND;
   return SRT_OK;
 }
@@ -1042,6 +1297,73 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
     std::memcpy(&w1, &n.prim_count, 4);
     hn[2 * (size_t)remap[i] + 2] = make_float4(n.min_bounds[0], n.min_bounds[1], n.min_bounds[2], w0);
     hn[2 * (size_t)remap[i] + 3] = make_float4(n.max_bounds[0], n.max_bounds[1], n.max_bounds[2], w1);
+  }
+  // Treelet scheduling (wavefront mode, wavefront.hpp): a copy of the node array in which every internal
+  // node at depth td of some tree (walked from every BVH root and from slot 0, where the ghost records
+  // start) is a treelet root -- its count kTreeletCnt, its child index the treelet's id -- and whose
+  // nodes with a treelet root as right child lose the right-spine flag (the top kernel must make the root
+  // current, not expand it).  Every path deeper than td passes a root, so the top-level stack holds < td
+  // entries.  Chosen for trees past the Infinity Cache, with ~1 MB treelets (SRT_TREELETS=1/0 forces it,
+  // SRT_TREELET_DEPTH sets td).
+  FreeDev(c->d_nodes_t);
+  FreeDev(c->d_troot);
+  c->d_nodes_t = nullptr;
+  c->d_troot = nullptr;
+  c->n_treelets = 0;
+  {
+    uint32_t max_leaf_in = 0;
+    for (uint32_t i = 0; i < n_nodes; ++i) max_leaf_in = std::max(max_leaf_in, nodes[i].prim_count);
+    int td = c->treelet_depth;
+    if (td == 0) {  // ~1 MB of nodes + triangles per treelet
+      td = 1;
+      while (td < srt::kTopStack - 1 && scene_mb / (double)(1u << (td + 1)) >= 1.0) ++td;
+    }
+    c->tl_scene = false;  // opt-in (measured slower than sample_kernel: DESIGN.md section 5, "Wavefront mode")
+    const bool want = c->treelets >= 0 ? c->treelets == 1 : c->tl_scene;
+    if (want && max_leaf_in < srt::kTreeletCnt && depth > td) {
+      std::vector<float4> hf(hn);
+      std::vector<uint32_t> troot;
+      std::vector<int32_t> tid_of(n_slots, -1);
+      auto u32 = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
+      auto f32 = [](uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; };
+      std::vector<uint32_t> roots{0};
+      for (uint32_t b = 0; b < n_bvhs; ++b) roots.push_back(remap[bvhs[b].first_index]);
+      std::vector<std::pair<uint32_t, int>> st;
+      const uint32_t ror = laid ? 1u : 0u;
+      for (uint32_t r : roots) {
+        st.push_back({r, 0});
+        while (!st.empty()) {
+          auto [sl, d] = st.back();
+          st.pop_back();
+          if (u32(hn[2 * (size_t)sl + 3].w) != 0u || tid_of[sl] >= 0) continue;  // a leaf, or a root already
+          const uint32_t first = u32(hn[2 * (size_t)sl + 2].w);
+          if (d == td) {
+            tid_of[sl] = (int32_t)troot.size();
+            troot.push_back(first);
+            hf[2 * (size_t)sl + 2].w = f32((uint32_t)tid_of[sl]);
+            hf[2 * (size_t)sl + 3].w = f32(srt::kTreeletCnt);
+            continue;
+          }
+          const uint32_t ref0 = first | ror;
+          st.push_back({ref0, d + 1});
+          st.push_back({ref0 + 1, d + 1});
+        }
+      }
+      for (uint32_t sl = 0; sl < n_slots && ror; ++sl) {  // no right-spine step onto a treelet root
+        const uint32_t first = u32(hn[2 * (size_t)sl + 2].w);
+        if (tid_of[sl] >= 0 || u32(hn[2 * (size_t)sl + 3].w) != 0u || (first & 1u)) continue;
+        if (first + 2 < n_slots && tid_of[first + 2] >= 0) hf[2 * (size_t)sl + 2].w = f32(first | 1u);
+      }
+      if (!troot.empty()) {
+        HIP_OK(hipMalloc(&c->d_nodes_t, hf.size() * sizeof(float4)));
+        HIP_OK(hipMalloc(&c->d_troot, troot.size() * sizeof(uint32_t)));
+        HIP_OK(hipMemcpyAsync(c->d_nodes_t, hf.data(), hf.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+        HIP_OK(hipMemcpyAsync(c->d_troot, troot.data(), troot.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                              c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
+        c->n_treelets = (uint32_t)troot.size();
+      }
+    }
   }
   // materials -> shading materials (raytrace_utils.glsl:140-175); one zero
   // record appended for out-of-range material indices (OOB SSBO reads = 0)

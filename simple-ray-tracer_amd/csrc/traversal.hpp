@@ -328,6 +328,9 @@ constexpr uint32_t kNoneRef = 0xFFFFFFFFu;
 // ref needs no update when a lane runs out of nodes.  Leaf counts are < 2^31
 // (srt_upload_scene validates it).
 constexpr uint32_t kNoneCnt = 0xFFFFFFFFu;
+// Wavefront mode's flagged node copy: the count of a treelet root (an internal node at the treelet
+// depth), whose child index holds the treelet's id instead (wavefront.hpp; leaves then hold < 255).
+constexpr uint32_t kTreeletCnt = 255u;
 __device__ __forceinline__ bool trav_at_leaf(uint32_t cnt) { return (int)cnt > 0; }
 #ifndef SRT_LEAF_TRIS
 #define SRT_LEAF_TRIS 2
@@ -534,9 +537,9 @@ __device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav
 // for both; then each kind's tests run on their lanes.  The memory-latency-bound
 // global mode trades the second kind's idle lanes for half the round trips;
 // each lane's steps, and so its decisions, are unchanged.
-template <bool COUNT, bool PACK, int RING = kShortStack>
+template <bool COUNT, bool PACK, int RING = kShortStack, bool TL = false>
 __device__ __forceinline__ void trav_fused(const KParams& kp, const Lane& ln, Counters& c, Trav& t, bool any) {
-  const bool at_int = t.cnt == 0u, at_leaf = trav_at_leaf(t.cnt);
+  const bool at_int = t.cnt == 0u, at_leaf = trav_at_leaf(t.cnt) && !(TL && t.cnt == kTreeletCnt);
   if (at_int | at_leaf) {
     const uint32_t ref0 = t.ref | kp.ref_or;
     const bool spine = kSpine<false> && at_int && (ref0 != t.ref);
@@ -605,13 +608,13 @@ __device__ __forceinline__ void trav_finish(const KParams& kp, Trav& t, bool any
   }
 }
 
-template <bool COUNT, bool LDSM, bool PACK, bool FUSE, int K, int RING = kShortStack>
+template <bool COUNT, bool LDSM, bool PACK, bool FUSE, int K, int RING = kShortStack, bool TL = false>
 __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln, Counters& c, Trav& t, bool any) {
   if constexpr (FUSE) {
     static_assert(!LDSM, "fused sub-steps are a global-scene mode schedule");
     if constexpr (K < kFusedSteps) {
-      trav_fused<COUNT, PACK, RING>(kp, ln, c, t, any);
-      trav_substeps<COUNT, LDSM, PACK, FUSE, K + 1, RING>(kp, ln, c, t, any);
+      trav_fused<COUNT, PACK, RING, TL>(kp, ln, c, t, any);
+      trav_substeps<COUNT, LDSM, PACK, FUSE, K + 1, RING, TL>(kp, ln, c, t, any);
     }
   } else if constexpr (step_kind<LDSM>(K) != 0) {
     if constexpr (step_kind<LDSM>(K) == 'I') {
@@ -619,11 +622,11 @@ __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln,
       if (t.cnt == 0) trav_internal<COUNT, LDSM, PACK, RING>(kp, ln, c, t);
     } else {
       DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K, trav_at_leaf(t.cnt));
-      if (trav_at_leaf(t.cnt)) trav_leaf<COUNT, LDSM>(kp, c, t, any);
+      if (trav_at_leaf(t.cnt) && !(TL && t.cnt == kTreeletCnt)) trav_leaf<COUNT, LDSM>(kp, c, t, any);
     }
     DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K + 2, t.active & (t.cnt == kNoneCnt));
     trav_pop<LDSM, PACK, RING>(kp, ln, t);
-    trav_substeps<COUNT, LDSM, PACK, FUSE, K + 1, RING>(kp, ln, c, t, any);
+    trav_substeps<COUNT, LDSM, PACK, FUSE, K + 1, RING, TL>(kp, ln, c, t, any);
   }
 }
 
@@ -633,12 +636,14 @@ __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln,
 // its own sequence per iteration, in order.  `any` selects the shadow-ray
 // (first hit) variant.
 // RING: global-scene mode's LDS ring entries per lane (a power of two).
-template <bool COUNT, bool LDSM, bool PACK, bool FUSE, int RING = kShortStack>
+// TL (wavefront mode's top-level kernel): a current node whose count is kTreeletCnt is a treelet root of
+// the flagged node copy; no sub-step takes it (the caller suspends the ray there, wavefront.hpp).
+template <bool COUNT, bool LDSM, bool PACK, bool FUSE, int RING = kShortStack, bool TL = false>
 __device__ __forceinline__ void trav_step(const KParams& kp, const Lane& ln, Counters& c, Trav& t, f3 ro, f3 rd,
                                           bool any) {
   static_assert((RING & (RING - 1)) == 0, "the LDS ring holds a power-of-two number of entries");
   if (t.start) trav_begin_bvh<COUNT, LDSM>(kp, c, t, ro, rd);  // only for BVHs after the first
-  trav_substeps<COUNT, LDSM, PACK, FUSE, 0, RING>(kp, ln, c, t, any);
+  trav_substeps<COUNT, LDSM, PACK, FUSE, 0, RING, TL>(kp, ln, c, t, any);
   trav_finish(kp, t, any);
 }
 
