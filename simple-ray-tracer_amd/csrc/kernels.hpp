@@ -366,22 +366,16 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : GW) void sample_kernel(KParams kp
 #endif
       const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
       const int samp = (kp.frame_first + frame_i) % kp.WH;
-      // row band of the tile when bands are whole tiles (the default 8 rows)
-      const int band_u = (kp.band_rows & 7) == 0 ? ty / (kp.band_rows >> 3) : -1;
       if (!has_work & !fresh & (r < avail)) {
         const int item = batch_next + r;
         const int px = tx * 8 + (item & 7), ly = ty * 8 + (item >> 3);
         if (px < kp.ext_w && ly < kp.local_rows) {
-          // global row of local row ly: the identity on one rank; else by the
-          // row band (whole tiles: per batch; power-of-two bands: a shift)
+          // global row of local row ly: the identity on one rank; else the row
+          // band's (kp.row_map, built by the host: a table read instead of the
+          // band arithmetic keeps the refill's code small -- it is shared with
+          // the traversal loop's registers, +0.7% on one rank)
           int yy = ly;
-          if (kp.nranks > 1) {
-            int band;
-            if (band_u >= 0) band = band_u;
-            else if (kp.band_shift >= 0) band = ly >> kp.band_shift;
-            else band = ly / kp.band_rows;
-            yy = (band * kp.nranks + kp.rank) * kp.band_rows + (ly - band * kp.band_rows);
-          }
+          if (kp.nranks > 1) yy = kp.row_map[ly];
           if (yy < kp.ext_h) {  // else the item is outside the dispatch extent: the lane tries the next one
             fresh = true;
             a_pl = px | (ly << 16);

@@ -126,6 +126,8 @@ struct srt_context {
   uint32_t* d_tile_order = nullptr;
   int tile_cap = 0, tile_costs_for = -1;
   bool tile_schedule = true;  // SRT_TILE_ORDER=0: natural tile order
+  int* d_row_map = nullptr;           // nranks > 1: global row of each local row (KParams::row_map)
+  long long row_map_key = -1;         // the (rank, nranks, band_rows, rows) it was built for
   unsigned long long* d_batch_ctr = nullptr;  // one batch counter per chunk launch
   int batch_ctr_cap = 0;
   size_t lbuf_bytes = 0;
@@ -337,6 +339,24 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
   for (int s = 0; s < 31; ++s)
     if ((1 << s) == c->band_rows) kp->band_shift = s;
   kp->local_rows = LocalRows(c, c->H);
+  if (c->nranks > 1) {  // the row bands' global rows, one table read per new sample in the kernels
+    const long long key = ((((long long)c->rank * 4096 + c->nranks) * 65536 + c->band_rows) << 20) + kp->local_rows;
+    if (key != c->row_map_key) {
+      std::vector<int> rows((size_t)std::max(kp->local_rows, 1));
+      for (int ly = 0; ly < kp->local_rows; ++ly) {
+        const int band = ly / c->band_rows;
+        rows[ly] = (band * c->nranks + c->rank) * c->band_rows + (ly - band * c->band_rows);
+      }
+      FreeDev(c->d_row_map);
+      c->d_row_map = nullptr;
+      c->row_map_key = -1;
+      HIP_OK(hipMalloc(&c->d_row_map, rows.size() * sizeof(int)));
+      HIP_OK(hipMemcpyAsync(c->d_row_map, rows.data(), rows.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+      HIP_OK(hipStreamSynchronize(c->stream));
+      c->row_map_key = key;
+    }
+    kp->row_map = c->d_row_map;
+  }
   kp->local_pixels = kp->local_rows * c->W;
   kp->ext_w = c->W;
   kp->ext_h = c->H;
@@ -1014,7 +1034,7 @@ int srt_destroy(srt_context* c) {
   FreeDev(c->d_nodes); FreeDev(c->d_tris); FreeDev(c->d_mats); FreeDev(c->d_bvhs); FreeDev(c->d_lights);
   FreeDev(c->d_tex); FreeDev(c->d_tex_info); FreeDev(c->d_tri_uv);
   FreeDev(c->d_noise_xy); FreeDev(c->d_noise_u); FreeDev(c->d_stats); FreeDev(c->d_nan); FreeDev(c->d_lbuf); FreeDev(c->d_gstack);
-  FreeDev(c->d_batch_ctr); FreeDev(c->d_tile_cost); FreeDev(c->d_tile_order);
+  FreeDev(c->d_batch_ctr); FreeDev(c->d_tile_cost); FreeDev(c->d_tile_order); FreeDev(c->d_row_map);
   FreeDev(c->d_wf_rec); FreeDev(c->d_wf_res); FreeDev(c->d_wf_state); FreeDev(c->d_wf_rayq); FreeDev(c->d_wf_hitq);
   FreeDev(c->d_wf_ctl); FreeDev(c->d_wf_items);
   FreeDev(c->d_nodes_t); FreeDev(c->d_troot); FreeDev(c->d_tl_ray); FreeDev(c->d_tl_stk); FreeDev(c->d_tl_slist);

@@ -321,19 +321,12 @@ __device__ __forceinline__ void pool_trace(const KParams& kp, Pool& P, Counters&
 #endif
       const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
       const int samp = (kp.frame_first + frame_i) % kp.WH;
-      const int band_u = (kp.band_rows & 7) == 0 ? ty / (kp.band_rows >> 3) : -1;
       if (!has & !fresh & (r < avail)) {
         const int item = batch_next + r;
         const int px = tx * 8 + (item & 7), ly = ty * 8 + (item >> 3);
         if (px < kp.ext_w && ly < kp.local_rows) {
           int yy = ly;
-          if (kp.nranks > 1) {
-            int band;
-            if (band_u >= 0) band = band_u;
-            else if (kp.band_shift >= 0) band = ly >> kp.band_shift;
-            else band = ly / kp.band_rows;
-            yy = (band * kp.nranks + kp.rank) * kp.band_rows + (ly - band * kp.band_rows);
-          }
+          if (kp.nranks > 1) yy = kp.row_map[ly];  // the row band's global row (as sample_kernel)
           if (yy < kp.ext_h) {
             fresh = true;
             a_pl = px | (ly << 16);

@@ -140,10 +140,7 @@ __device__ __forceinline__ bool wf_item_pixel(const KParams& kp, uint32_t item, 
   const int px = tx * 8 + (k & 7), ly = ty * 8 + (k >> 3);
   if (px >= kp.ext_w || ly >= kp.local_rows) return false;
   int yy = ly;
-  if (kp.nranks > 1) {
-    const int band = kp.band_shift >= 0 ? ly >> kp.band_shift : ly / kp.band_rows;
-    yy = (band * kp.nranks + kp.rank) * kp.band_rows + (ly - band * kp.band_rows);
-  }
+  if (kp.nranks > 1) yy = kp.row_map[ly];  // the row band's global row
   if (yy >= kp.ext_h) return false;
   pl = px | (ly << 16);
   gy = yy;
