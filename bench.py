@@ -333,7 +333,7 @@ def timed_kernel(run, scene: str) -> str:
     if scene == "rubik":
         return KERNEL_LDS
     if scene == "spheres":
-        return "srt::sample_kernel<false, false, true, 256, false, false, 4> (spheres: no BVH)"
+        return "srt::sphere_kernel<false> (spheres: no BVH, 3 waves per SIMD)"
     fused = run.c.GetInt("scene.fused") == 1
     gw = run.c.GetInt("scene.global_waves") if fused else 4
     return (f"srt::sample_kernel<false, false, true, 256, false, {'true' if fused else 'false'}, {gw}> "

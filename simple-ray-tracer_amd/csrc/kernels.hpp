@@ -47,14 +47,15 @@ __host__ __device__ constexpr int global_ring(int gw) { return gw > 4 ? 8 : kSho
 // Returns what the path traces next: kShadeShadow (CheckLightOccluded's ray, ro/rd/tmax set,
 // the bounce direction in nd), kShadeBounce (the next CheckHit ray) or kShadeDone.
 enum { kShadeDone = 0, kShadeShadow = 1, kShadeBounce = 2 };
-template <bool COUNT, bool LDSM, bool TEX>
+// SPH: the sphere scene's instance (sphere_kernel); every other caller is a mesh scene (showModel set).
+template <bool COUNT, bool LDSM, bool TEX, bool SPH = false>
 __device__ __forceinline__ int shade_hit(const KParams& kp, const Lane& ln, Counters& c, uint32_t ht, int hit_sphere,
                                          float dist, f3& ro, f3& rd, float& tmax, f3& T, int& depth, int& randIndex,
                                          int& bounces, bool& term, f3& q0, f3& q1, f3& nd) {
   // ---- hit record (CheckHit) ----
   Hit rec;
   rec.hit = true;
-  if (kp.show_model) {
+  if constexpr (!SPH) {
     rec.p = (dist * rd) + ro;
     const float4* tp = tri_ptr<LDSM>(kp, ht);
     const float4 A = tp[0], B = tp[1], C = tp[2];
@@ -230,8 +231,11 @@ __device__ __forceinline__ int shade_hit(const KParams& kp, const Lane& ln, Coun
 // mode, where the 1024-thread block's LDS caps residency at 4 anyway; GW in
 // global-scene mode (see global_ring), whose memory latency wants more waves
 // FUSE: global-scene mode's fused sub-steps (trav_fused) instead of kStepPattern
-template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX, bool FUSE, int GW = 4>
-__global__ __launch_bounds__(BLOCK, LDSM ? 4 : GW) void sample_kernel(KParams kp) {
+// sample_kernel's body.  SPH: the sphere scene (showModel false: the five spheres, no BVH); otherwise a
+// mesh scene (showModel set).  Each instance holds only its scene kind's code, so neither carries the
+// other's registers beside its loop.
+template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX, bool FUSE, int GW, bool SPH>
+__device__ __forceinline__ void sample_body(const KParams& kp) {
   const int tid = threadIdx.x;
 #ifdef SRT_WAVE_TRACE
   const unsigned long long tw0 = __builtin_amdgcn_s_memrealtime();
@@ -308,7 +312,7 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : GW) void sample_kernel(KParams kp
     tr.active = true;
     tr.start = false;
     bump<COUNT>(c, ST_RAYS);
-    if (kp.show_model) {
+    if constexpr (!SPH) {
       trav_begin_bvh<COUNT, LDSM>(kp, c, tr, ro, rd);
       if (tr.cnt == kNoneCnt) {  // root box missed: next BVH, or done
         if (kp.bvh_count > 1) tr.start = true, tr.bi = 1;
@@ -437,7 +441,7 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : GW) void sample_kernel(KParams kp
     PHASE_STAMP(t_b);
 
     // ---- (B) traverse until too few lanes are still traversing ----
-    if (kp.show_model) {
+    if constexpr (!SPH) {
       // has_work is fixed during traversal; trav_frac16 <= 16 makes
       // n_trav * 16 < n_work * trav_frac16 imply n_trav < n_work
       const int work_lim = __popcll(__ballot(has_work)) * kp.trav_frac16;
@@ -462,7 +466,7 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : GW) void sample_kernel(KParams kp
 #endif
     // ---- (C) lanes whose ray returned: shade (GetRayColor's loop body) ----
     if (has_work && !tr.active) {
-      const bool hit = kp.show_model ? (tr.hit != kNoneRef) : (hit_sphere >= 0);
+      const bool hit = !SPH ? (tr.hit != kNoneRef) : (hit_sphere >= 0);
       const float dist = tr.dist;
       if (shadow_phase) {  // CheckLightOccluded returned: this bounce's direct light
         color = color + (hit ? q0 : q1);
@@ -477,8 +481,8 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : GW) void sample_kernel(KParams kp
       } else if (!hit) {
         finish_sample();
       } else {
-        const int next = shade_hit<COUNT, LDSM, TEX>(kp, ln, c, tr.hit, hit_sphere, dist, ro, rd, tmax, T, depth,
-                                                     randIndex, bounces, term, q0, q1, nd);
+        const int next = shade_hit<COUNT, LDSM, TEX, SPH>(kp, ln, c, tr.hit, hit_sphere, dist, ro, rd, tmax, T,
+                                                          depth, randIndex, bounces, term, q0, q1, nd);
         if (next == kShadeDone) {
           finish_sample();
         } else {
@@ -519,6 +523,19 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : GW) void sample_kernel(KParams kp
   }
 #endif
   flush_counters<COUNT>(kp, c);
+}
+
+// A mesh scene (showModel set); FUSE/GW: global-scene mode's schedule and waves per SIMD.
+template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX, bool FUSE, int GW = 4>
+__global__ __launch_bounds__(BLOCK, LDSM ? 4 : GW) void sample_kernel(KParams kp) {
+  sample_body<COUNT, LDSM, PACK, BLOCK, TEX, FUSE, GW, false>(kp);
+}
+
+// The sphere scene (SHOW_MODEL 0, raytrace_compute.glsl:299-364): the same loop, each ray testing the
+// five spheres in one go.
+template <bool COUNT>
+__global__ __launch_bounds__(256, 4) void sphere_kernel(KParams kp) {
+  sample_body<COUNT, false, true, 256, false, false, 4, true>(kp);
 }
 
 // Schedule of the next sample_kernel launch: its n tiles by decreasing cost

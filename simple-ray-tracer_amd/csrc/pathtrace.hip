@@ -144,6 +144,7 @@ struct srt_context {
   int pool_slots_max = 4096;           // SRT_POOL_SLOTS: at most this many records
   int pool_deadline_ms = 30000;        // SRT_POOL_DEADLINE_MS: pool_kernel's watchdog
   int num_cus = 256;
+  int sphere_blocks = 3;               // SRT_SPHERE_BLOCKS: sphere_kernel blocks per CU
   // wavefront mode (wavefront.hpp): global-scene launches through wf_logic / wf_shade / wf_trace
   int wavefront = -1;                  // SRT_WAVEFRONT=1/0 forces it on / off; -1: by scene (wf_scene)
   bool wf_scene = false;               // chosen at upload
@@ -431,12 +432,41 @@ int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
   return SRT_OK;
 }
 
+// The sphere scene (showModel false): sphere_kernel, one 256-lane block per resident slot (no stacks,
+// so its LDS holds only the light records).
+template <bool COUNT>
+int LaunchSpheres(srt_context* c, srt::KParams kp, size_t lds) {
+  const void* fn = reinterpret_cast<const void*>(&srt::sphere_kernel<COUNT>);
+  int per_cu = 0;
+  for (const auto& e : c->occupancy)
+    if (e.fn == fn && e.lds == lds) per_cu = e.per_cu;
+  if (per_cu == 0) {
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sphere_kernel<COUNT>, 256, lds));
+    per_cu = std::max(per_cu, 1);
+    c->occupancy.push_back({fn, lds, per_cu});
+  }
+  // resident blocks per CU: the sphere loop runs best at 3 waves per SIMD (C2 on one box, ms per launch:
+  // 3 blocks 5.75, 4 5.88, 5 6.19, 6 6.24; its 87 VGPRs would allow 5); SRT_SPHERE_BLOCKS sets it
+  const int blocks = c->num_cus * std::min(per_cu, c->sphere_blocks);
+  {
+    const long long waves = (long long)blocks * 4;
+    const long long n_batches = (long long)((kp.W + 7) >> 3) * ((kp.local_rows + 7) >> 3) * kp.nframes;
+    kp.tail_start = (int)std::max<long long>(0, n_batches - (long long)c->tail_claims * srt::kClaim * waves);
+  }
+  HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
+  hipLaunchKernelGGL(srt::sphere_kernel<COUNT>, dim3(blocks), dim3(256), lds, c->stream, kp);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
+  return SRT_OK;
+}
+
 // The sample_kernel instance for the launch: counting or not, LDS-resident
 // scene or global (packed stack entries when indices fit 24 bits; the timed
 // global instance's schedule and waves per SIMD chosen at upload), and with
 // or without the texture-sampling branch (TEX, only when a material samples).
 template <bool TEX>
 int LaunchMode(srt_context* c, const srt::KParams& kc, size_t lds, bool count, bool ldsm, bool pack) {
+  if (!kc.show_model) return count ? LaunchSpheres<true>(c, kc, lds) : LaunchSpheres<false>(c, kc, lds);
   if (count && ldsm) return LaunchSamples<true, true, true, 1024, TEX>(c, kc, lds);
   if (count) return pack ? LaunchSamples<true, false, true, 256, TEX>(c, kc, lds)
                          : LaunchSamples<true, false, false, 256, TEX>(c, kc, lds);
@@ -706,10 +736,13 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
     } else if (ldsm) {
       kp.stack_base_f4 = kp.nodes_lds_f4 + kp.tris_f4;
       lds = lds_mode_bytes;
-    } else {  // LDS rings of global_ring(waves) entries per lane, backed by HBM stacks (LaunchSamples)
+    } else if (kp.show_model) {  // LDS rings of global_ring(waves) entries per lane, backed by HBM stacks
       kp.stack_base_f4 = 0;
       const int gw = (!count && c->fused) ? c->global_waves : 4;  // LaunchMode's instance
       lds = (size_t)block * (c->lds_ok ? 2 : 3) * sizeof(uint32_t) * (size_t)srt::global_ring(gw);
+    } else {  // the sphere scene (sphere_kernel): no traversal stacks
+      kp.stack_base_f4 = 0;
+      lds = 0;
     }
     {  // light and material records in LDS behind the rest, when they fit (shading reads them there)
       lds = (lds + 15) & ~(size_t)15;
@@ -987,6 +1020,7 @@ int srt_create(int device, void* stream, srt_context** out) {
   if (const char* e = std::getenv("SRT_POOL_TLOW")) c->pool_tlow = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("SRT_POOL_SLOTS")) c->pool_slots_max = std::max(64, std::atoi(e));
   if (const char* e = std::getenv("SRT_POOL_DEADLINE_MS")) c->pool_deadline_ms = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("SRT_SPHERE_BLOCKS")) c->sphere_blocks = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("SRT_WAVEFRONT")) c->wavefront = e[0] == '1' ? 1 : 0;
   if (const char* e = std::getenv("SRT_WF_SLOTS")) c->wf_slots = (uint32_t)std::max(256L, std::min(1L << 28, std::atol(e)));
   if (const char* e = std::getenv("SRT_WF_WAVES")) c->wf_waves = std::atoi(e);

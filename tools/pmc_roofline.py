@@ -3,7 +3,8 @@
 usage: python tools/pmc_roofline.py gpurun_out/r02 [--tag r02] [--workload NAME]
 (--workload: a single-leg run, e.g. tools/pmc_c5.sh's, whose global-scene instance is NAME; --il: that
 run took the IL-pattern instance, as trees past 600 MB do; --sum: sum every non-counting sample_kernel
-dispatch of a single-workload run, whatever its instance, e.g. tools/pmc_configs.sh's C2 and C4)
+(or sphere_kernel) dispatch of a single-workload run, whatever its instance, e.g. tools/pmc_configs.sh's
+C2 and C4)
 
 Each pass ran `python bench.py --steps 1 --warmup 0 --no-cpu-baseline`, so every leg's timed step
 launched its sample_kernel<false, ...> instance exactly once (the counting run is the <true, ...>
@@ -39,7 +40,7 @@ if only:  # the one timed global-scene instance of the run, whatever its waves p
 SUM = "--sum" in sys.argv
 if SUM:
     assert only, "--sum needs --workload"
-    LEGS = {"void srt::sample_kernel<false, ": [only]}
+    LEGS = {("void srt::sample_kernel<false, ", "void srt::sphere_kernel<false>"): [only]}
 
 
 def rows(sub):
@@ -51,7 +52,7 @@ def per_launch(sub):
     """{workload: {counter: value}} of each leg's dispatch (summed over the dimensions rocprofv3 splits)."""
     out = {}
     for leg_kernel, wls in LEGS.items():
-        rs = [r for r in rows(sub) if r["Kernel_Name"].startswith(leg_kernel)]
+        rs = [r for r in rows(sub) if r["Kernel_Name"].startswith(leg_kernel)]  # (str.startswith takes a tuple)
         if SUM:
             agg = {}
             for r in rs:
