@@ -156,6 +156,7 @@ struct srt_context {
            *d_wf_items = nullptr;
   uint32_t wf_cap = 0;
   uint32_t* h_wf_poll = nullptr;       // pinned: (live, items) of two polled iterations
+  hipEvent_t wf_poll_ev[2] = {nullptr, nullptr};
   bool wf_launched = false;            // the last render went through wavefront mode
   // treelet scheduling of wavefront mode's trace stage (wavefront.hpp wf_top_kernel / wf_bottom_kernel)
   int treelets = -1;                   // SRT_TREELETS=1/0 forces it on / off; -1: by scene (tl_scene)
@@ -667,9 +668,11 @@ int LaunchWavefront(srt_context* c, srt::KParams kp, bool tex) {
     kp.gstack_stride = kt.gstack_stride = (int)lanes;
   }
   const dim3 sgrid((P + 255) / 256);
-  hipEvent_t poll_ev[2];
-  HIP_OK(hipEventCreateWithFlags(&poll_ev[0], hipEventDisableTiming));
-  HIP_OK(hipEventCreateWithFlags(&poll_ev[1], hipEventDisableTiming));
+  if (!c->wf_poll_ev[0]) {
+    HIP_OK(hipEventCreateWithFlags(&c->wf_poll_ev[0], hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&c->wf_poll_ev[1], hipEventDisableTiming));
+  }
+  hipEvent_t* poll_ev = c->wf_poll_ev;
   HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
   int it = 0;
   bool done = false;
@@ -695,8 +698,6 @@ int LaunchWavefront(srt_context* c, srt::KParams kp, bool tex) {
       }
     }
   }
-  (void)hipEventDestroy(poll_ev[0]);
-  (void)hipEventDestroy(poll_ev[1]);
   if (rc) return rc;
   if (!done) {
     srt::SetError("wavefront mode: iteration limit reached");
@@ -1074,6 +1075,8 @@ int srt_destroy(srt_context* c) {
   FreeDev(c->d_nodes_t); FreeDev(c->d_troot); FreeDev(c->d_tl_ray); FreeDev(c->d_tl_stk); FreeDev(c->d_tl_slist);
   FreeDev(c->d_tl_skey); FreeDev(c->d_tl_blist); FreeDev(c->d_tl_rlist); FreeDev(c->d_tl_count); FreeDev(c->d_tl_fill);
   if (c->h_wf_poll) (void)hipHostFree(c->h_wf_poll);
+  for (hipEvent_t e : c->wf_poll_ev)
+    if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (!c->images_external) { FreeDev(c->d_accum); FreeDev(c->d_out); }
   if (c->own_stream) (void)hipStreamDestroy(c->stream);

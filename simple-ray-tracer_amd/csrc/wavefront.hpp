@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void wf_logic_kernel(KParams kp, WfParams w) {
   uint32_t* ctl = w.ctl + (size_t)WQ_WORDS * (size_t)w.iter;
   const int lane = threadIdx.x & 63;
   uint32_t st = valid ? w.state[s] : (uint32_t)WF_NONE;
-  bool want = st == WF_EMPTY, trace = false, shade = false, shadow = false;
+  bool want = st == WF_EMPTY, trace = false, shade = false;  // (only wf_shade_kernel starts shadow rays)
   if (st == WF_RET) {
     WfPath r = wf_load(w, s);
     const uint2 res = w.res[s];
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void wf_logic_kernel(KParams kp, WfParams w) {
       if (want) {
         const uint32_t item = base + (uint32_t)lane_rank(m, lane);
         int pl = 0, gy = 0, fi = 0, samp = 0;
-        if (item >= base && item < w.n_items && wf_item_pixel(kp, item, pl, gy, fi, samp)) {
+        if (item < w.n_items && wf_item_pixel(kp, item, pl, gy, fi, samp)) {
           const int x = pl & 0xFFFF;
           // GetRay (raytrace_compute.glsl:78-90) with SampleSquare (raytrace_utils.glsl:10-17)
           const float2 nz = kp.noise_xy[wrap_index(gy * kp.H + x + samp, kp.WH)];
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(256) void wf_logic_kernel(KParams kp, WfParams w) {
     else if (shade) w.state[s] = WF_HIT;
     else if (st == WF_RET || want) w.state[s] = WF_EMPTY;
   }
-  wf_append(&ctl[WQ_RAYS], w.rayq, trace, s | (shadow ? kWfShadowBit : 0u));
+  wf_append(&ctl[WQ_RAYS], w.rayq, trace, s);
   wf_append(&ctl[WQ_HITS], w.hitq, shade, s);
   const unsigned long long live = __ballot(trace || shade || (valid && st == WF_TRACE) || (valid && st == WF_HIT));
   if (live != 0ull && lane == __ffsll((long long)live) - 1) atomicAdd(&ctl[WQ_LIVE], (uint32_t)__popcll(live));
