@@ -138,9 +138,11 @@ int srt_nan_samples(srt_context* ctx, uint64_t* out);
 int srt_set_tiling(srt_context* ctx, int rank, int nranks, int band_rows);
 int srt_local_rows(srt_context* ctx);
 /* The context's HIP device, and a uniform's current value (glGetUniformiv): the int / uint / bool
- * uniforms above by name; SRT_ERR_NOT_FOUND for other names.  Two read-only names report what the
+ * uniforms above by name; SRT_ERR_NOT_FOUND for other names.  Read-only names report what the
  * uploaded scene's size chose for global-scene mode's timed kernel: "scene.fused" (1: fused
- * sub-steps, 0: the IL pattern) and "scene.global_waves" (waves per SIMD of the fused instance). */
+ * sub-steps, 0: the IL pattern), "scene.global_waves" (waves per SIMD of the fused instance) and
+ * "scene.tri_slots" (device triangle records: more than the scene's triangles when small leaves
+ * are laid out line by line for a tree streamed from HBM). */
 int srt_device(srt_context* ctx);
 int srt_get_int(srt_context* ctx, const char* name, int* v);
 

@@ -641,7 +641,8 @@ __global__ __launch_bounds__(256) void closest_kernel(KParams kp, const srt_ray*
                                       xform(rec.frame, d, 0.0f), dist, false);
     if (h != 0xFFFFFFFFu) hit = h;
   }
-  hits[i] = hit;
+  // the hit record's input triangle index (its slot differs under LayoutTris)
+  hits[i] = hit == 0xFFFFFFFFu ? hit : __float_as_uint(kp.tris[3 * (size_t)hit + 2].z);
   tout[i] = dist;
   flush_counters<true>(kp, c);
 }

@@ -993,6 +993,44 @@ bool LayoutNodes(const srt_bvh_node* nodes, uint32_t n_nodes, const srt_bvh_reco
   return true;
 }
 
+// Device triangle slots for scenes read through L2 (global-scene mode).  A leaf
+// of one or two triangles (the midpoint builder's leaves on a triangle soup) is
+// read by one leaf step; at 48 B per record, 5 of every 8 such reads straddle
+// two 128-B lines.  Here each such leaf starts at a slot whose records
+// lie in one line (slot mod 8 in {0, 1, 3, 4, 6, 7} for one record, {0, 3, 6}
+// for two), zero records filling the gaps; larger leaves are not padded.  The
+// map is monotone, so the order is kept and a BVH's triangle range stays one
+// slot range.  Returns false (identity) when two leaves' ranges partly overlap.
+bool LayoutTris(const srt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_tris, std::vector<uint32_t>* slot,
+                uint32_t* n_slots) {
+  constexpr uint32_t kUnset = 0xFFFFFFFFu;
+  std::vector<uint32_t> owner(n_tris, kUnset), lead(n_tris, 0);
+  for (uint32_t i = 0; i < n_nodes; ++i) {
+    const srt_bvh_node& n = nodes[i];
+    if (n.prim_count == 0) continue;
+    const uint32_t f = n.first_child_or_prim_index;
+    if (lead[f] != 0 && lead[f] != n.prim_count) return false;  // two leaves from one triangle, different sizes
+    if (lead[f] == n.prim_count) continue;                      // the same leaf again (a shared subtree)
+    for (uint32_t t = f; t < f + n.prim_count; ++t) {
+      if (owner[t] != kUnset) return false;
+      owner[t] = f;
+    }
+    lead[f] = n.prim_count;
+  }
+  slot->resize(n_tris);
+  uint32_t s = 0;
+  for (uint32_t t = 0; t < n_tris; ++t) {
+    if (lead[t] == 1) {
+      while ((s & 7u) == 2u || (s & 7u) == 5u) ++s;
+    } else if (lead[t] == 2) {
+      while ((s & 7u) % 3u != 0u) ++s;  // {0, 3, 6}
+    }
+    (*slot)[t] = s++;
+  }
+  *n_slots = s;
+  return true;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -1165,6 +1203,7 @@ int srt_get_int(srt_context* c, const char* name, int* v) {
   else if (n == "scene.wavefront") *v = c->wavefront >= 0 ? c->wavefront : (c->wf_scene ? 1 : 0);
   else if (n == "scene.wf_waves") *v = c->wf_waves;
   else if (n == "scene.treelets") *v = (int)c->n_treelets;
+  else if (n == "scene.tri_slots") *v = (int)c->n_tris;  // device triangle records (LayoutTris gaps included)
   else return SRT_ERR_NOT_FOUND;
   return SRT_OK;
 }
@@ -1327,6 +1366,19 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   const char* gw_env = std::getenv("SRT_GLOBAL_WAVES_MODE");
   c->global_waves = gw_env ? (gw_env[0] == '5' ? 5 : 4) : (scene_mb < 48.0 ? 5 : 4);
   bool laid = !(lay_env && lay_env[0] == '0') && LayoutNodes(nodes, n_nodes, bvhs, n_bvhs, align, &remap, &n_slots);
+  // Triangle slots (LayoutTris) for every scene read through L2 (none of 1 MB fits the LDS copy):
+  // fewer lines per leaf step (A/B on one box, kernel ms: C5 10 M 4096² 820 -> 773 with the IL leaf
+  // step's own-record reads, 3 M 58.4 -> 56.5, 1 M 34.1 -> 32.6, torus knot 27.4 -> 27.4, Rubik
+  // unchanged).  SRT_TRI_ALIGN=1/0 forces either.  Leaves and each BVH's triangle range are
+  // remapped; a record keeps its triangle's input index (C.z) for the closest-hit query.
+  const char* ta_env = std::getenv("SRT_TRI_ALIGN");
+  const bool tri_align = ta_env ? ta_env[0] == '1' : scene_mb >= 1.0;
+  std::vector<uint32_t> tslot;
+  uint32_t n_tslots = n_tris;
+  const bool tris_laid = tri_align && LayoutTris(nodes, n_nodes, n_tris, &tslot, &n_tslots);
+  auto tsl = [&](uint32_t t) { return tris_laid ? tslot[t] : t; };
+  for (auto& r : tri_ranges)
+    if (r.first < r.second) r = {tsl(r.first), tsl(r.second - 1) + 1};
   if (!laid) {
     remap.resize(n_nodes);
     for (uint32_t i = 0; i < n_nodes; ++i) remap[i] = i;
@@ -1348,6 +1400,8 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
       first = remap[first];
       if (laid && n1.prim_count == 0 && remap[n1.first_child_or_prim_index] == remap[c0] + 2) first -= 1;
       if (((first | (laid ? 1u : 0u)) & 1u) == 0) pairs_aligned = false;  // overlapping sibling pairs
+    } else {
+      first = tsl(first);
     }
     float w0, w1;
     std::memcpy(&w0, &first, 4);
@@ -1445,11 +1499,12 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
     hm[2 * (size_t)i] = make_float4(alb[0], alb[1], alb[2], rough);
     hm[2 * (size_t)i + 1] = make_float4(m.specular[0], m.specular[1], m.specular[2], tf);
   }
-  // triangles: v0, e1 = v1 - v0, e2 = v2 - v0, material
+  // triangles (at their slots): v0, e1 = v1 - v0, e2 = v2 - v0, material, input index
   // kTriPad zero records past the end: a multi-triangle leaf step may read (and discard) them
-  std::vector<float4> ht(3 * ((size_t)n_tris + srt::kTriPad), make_float4(0, 0, 0, 0));
+  std::vector<float4> ht(3 * ((size_t)n_tslots + srt::kTriPad), make_float4(0, 0, 0, 0));
   auto vert = [&](uint32_t i, int k) -> float { return i < n_verts ? verts[i].vertex[k] : 0.0f; };
   for (uint32_t t = 0; t < n_tris; ++t) {
+    const size_t st = tsl(t);
     const srt_triangle& tr = tris[t];
     float v0[3], e1[3], e2[3];
     for (int k = 0; k < 3; ++k) {
@@ -1458,21 +1513,23 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
       e2[k] = vert(tr.v2_idx, k) - v0[k];
     }
     const uint32_t mi = tr.material_idx < n_mats ? tr.material_idx : n_mats;
-    float mf;
+    float mf, tf;
     std::memcpy(&mf, &mi, 4);
-    ht[3 * (size_t)t + 0] = make_float4(v0[0], v0[1], v0[2], e1[0]);
-    ht[3 * (size_t)t + 1] = make_float4(e1[1], e1[2], e2[0], e2[1]);
-    ht[3 * (size_t)t + 2] = make_float4(e2[2], mf, 0.0f, 0.0f);
+    std::memcpy(&tf, &t, 4);
+    ht[3 * st + 0] = make_float4(v0[0], v0[1], v0[2], e1[0]);
+    ht[3 * st + 1] = make_float4(e1[1], e1[2], e2[0], e2[1]);
+    ht[3 * st + 2] = make_float4(e2[2], mf, tf, 0.0f);
   }
   // vertex uvs per triangle, for the materials that sample a texture
   std::vector<float4> huv;
   if (sampled) {
-    huv.assign(2 * (size_t)n_tris, make_float4(0, 0, 0, 0));
+    huv.assign(2 * (size_t)n_tslots, make_float4(0, 0, 0, 0));
     auto uv = [&](uint32_t i, int k) -> float { return i < n_verts ? verts[i].texture[k] : 0.0f; };
     for (uint32_t t = 0; t < n_tris; ++t) {
       const srt_triangle& tr = tris[t];
-      huv[2 * (size_t)t] = make_float4(uv(tr.v0_idx, 0), uv(tr.v0_idx, 1), uv(tr.v1_idx, 0), uv(tr.v1_idx, 1));
-      huv[2 * (size_t)t + 1] = make_float4(uv(tr.v2_idx, 0), uv(tr.v2_idx, 1), 0.0f, 0.0f);
+      const size_t st = tsl(t);
+      huv[2 * st] = make_float4(uv(tr.v0_idx, 0), uv(tr.v0_idx, 1), uv(tr.v1_idx, 0), uv(tr.v1_idx, 1));
+      huv[2 * st + 1] = make_float4(uv(tr.v2_idx, 0), uv(tr.v2_idx, 1), 0.0f, 0.0f);
     }
   }
   FreeDev(c->d_nodes); FreeDev(c->d_mats); FreeDev(c->d_tris); FreeDev(c->d_tri_uv);
@@ -1496,12 +1553,12 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   c->bvhs_dirty = true;
   c->n_nodes = n_slots + srt::kNodePad;
   c->ref_or = laid ? 1u : 0u;
-  c->n_tris = n_tris;
+  c->n_tris = n_tslots;  // device records (slots)
   c->n_mats = n_mats;
   c->stack_entries = depth + 1;
   uint32_t max_leaf = 0;
   for (uint32_t i = 0; i < n_nodes; ++i) max_leaf = std::max(max_leaf, nodes[i].prim_count);
-  c->lds_ok = n_tris < (1u << 24) && n_slots + srt::kNodePad < (1u << 24) && max_leaf < 256;
+  c->lds_ok = n_tslots < (1u << 24) && n_slots + srt::kNodePad < (1u << 24) && max_leaf < 256;
   c->pairs_aligned = pairs_aligned;
   c->scene_ok = true;
   if (c->bvh_count == 0) c->bvh_count = n_bvhs;

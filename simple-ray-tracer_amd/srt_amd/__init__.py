@@ -418,7 +418,8 @@ class Compute:
             self.height = int(val)
 
     def GetInt(self, name: str) -> int:
-        """An int / uint / bool uniform's value, or "scene.fused" / "scene.global_waves" (srt_get_int)."""
+        """An int / uint / bool uniform's value, or a scene choice: "scene.fused", "scene.global_waves",
+        "scene.tri_slots" (srt_get_int)."""
         v = C.c_int()
         check(lib().srt_get_int(self.ctx, name.encode(), C.byref(v)), f"GetInt({name})")
         return v.value

@@ -231,6 +231,53 @@ def test_node_layouts_global_mode(monkeypatch, env):
     assert_parity(two, 2)
 
 
+@pytest.mark.parametrize("env", [{"SRT_TRI_ALIGN": "1", "SRT_NODE_ALIGN": "1", "SRT_GLOBAL_FUSED_MODE": "0"},
+                                 {"SRT_TRI_ALIGN": "1", "SRT_GLOBAL_FUSED_MODE": "1"},
+                                 {"SRT_TRI_ALIGN": "1", "SRT_NODE_LAYOUT": "0", "SRT_GLOBAL_FUSED_MODE": "0"},
+                                 {"SRT_TRI_ALIGN": "1"},
+                                 {"SRT_TRI_ALIGN": "0", "SRT_GLOBAL_FUSED_MODE": "0"}])
+def test_triangle_slots(monkeypatch, tmp_path, rubik, env):
+    """Line-aligned triangle slots (pathtrace.hip LayoutTris, chosen for every scene of 1 MB or more):
+    gaps of zero records between small leaves, leaf and BVH triangle ranges remapped.  Global mode on
+    both schedules and the LDS kernel (Rubik, forced) render the oracle's frame; a moved second model and
+    sampled textures (the hit's BVH found by its slot range) too; the closest-hit query returns input
+    triangle indices.  The identity layout (forced) is checked the same way."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    soup = R.make_setup(48, 40, show_model=True, models=[R.synthetic_model(30000, seed=3)])
+    r = R.Renderer(soup)
+    try:
+        slots = r.compute.GetInt("scene.tri_slots")
+        # the soup's 1- and 2-triangle leaves leave gaps
+        assert slots == 30000 if env["SRT_TRI_ALIGN"] == "0" else slots > 30000
+    finally:
+        r.close()
+    assert_parity(soup, 2)
+    two = R.make_setup(40, 32, show_model=True, models=[R.synthetic_model(20000, seed=4),
+                                                        R.synthetic_model(5000, seed=6)])
+    frame = np.eye(4, dtype=np.float32)
+    frame[3, :3] = (1.5, -2.0, 0.5)
+    two.scene.bvhs[1]["frame"] = frame.reshape(16)
+    assert_parity(two, 2)
+    obj = _textured_obj(tmp_path)
+    tex = R.make_setup(48, 40, show_model=True, models=[S.load_obj(obj, texcoords=True),
+                                                        S.load_obj(obj, texcoords=True)], bvh_count=3)
+    tex.scene.bvhs[1]["frame"] = frame.reshape(16)
+    assert_parity(tex, 2)
+    assert_parity(R.make_setup(64, 48, show_model=True, models=[rubik]), 2)
+    for scene, n in ((S.Scene.from_models([rubik]), 20000), (soup.scene, 4000)):
+        rays = _kat_rays(n, 11)
+        hits_o, t_o, _, _ = O.Oracle(scene).trace_closest(1, rays)
+        c = S.Compute().Init()
+        try:
+            c.bind_scene(scene)
+            c.SetUInt("bvh_count", 1)
+            hits, t = c.trace_closest(rays)
+        finally:
+            c.close()
+        assert (hits == hits_o).all() and bits_equal(t, t_o).all()
+
+
 def test_global_schedule_chosen_by_scene_size():
     """srt_upload_scene's choices for the timed global-scene instance, as bench.py reports them: the torus
     knot (20 MB of nodes + triangles) takes fused sub-steps at 5 waves per SIMD, a 1 M soup (101 MB)
