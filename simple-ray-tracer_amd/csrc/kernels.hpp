@@ -34,6 +34,11 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
 #ifndef SRT_TILE_SCHED
 #define SRT_TILE_SCHED 1  // tiles of each frame in the last launch's cost order
 #endif
+// The IL instance (trees past 600 MB) deals a tile's frames in a row (C5 783 -> 771 ms per launch,
+// A/B on one box; 8 or 16 batches per claim instead of 4: 776 / 792 ms)
+#ifndef SRT_TILE_MAJOR_IL
+#define SRT_TILE_MAJOR_IL 1
+#endif
 
 // Global-scene mode's occupancy regimes (GW, waves per SIMD): 4 (<= 128 VGPRs, no
 // spills; 16-entry LDS rings, 32 KiB per 256-lane block), or 5 (<= 96 VGPRs, ~10
@@ -361,8 +366,11 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
       // batch): frame by frame, and within a frame the tiles in tile_order (the
       // last launch's tiles by decreasing cost, order_tiles_kernel), read by a
       // scalar load (constant address space: the order is read-only here)
-      const int frame_i = batch / n_tiles;
-      const int trank = batch - frame_i * n_tiles;
+      // the IL instance deals a tile's frames in a row (SRT_TILE_MAJOR_IL): a claim's batches then
+      // trace the same pixels' camera rays, whose paths' lines are still in L2
+      constexpr bool kTileMajor = SRT_TILE_MAJOR_IL && !LDSM && !FUSE && !SPH;
+      const int frame_i = kTileMajor ? batch % kp.nframes : batch / n_tiles;
+      const int trank = kTileMajor ? batch / kp.nframes : batch - frame_i * n_tiles;
 #if SRT_TILE_SCHED
       const int tile = (int)((const __attribute__((address_space(4))) uint32_t*)(kp.tile_order))[trank];
 #else

@@ -1375,7 +1375,8 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   const bool tri_align = ta_env ? ta_env[0] == '1' : scene_mb >= 1.0;
   std::vector<uint32_t> tslot;
   uint32_t n_tslots = n_tris;
-  const bool tris_laid = tri_align && LayoutTris(nodes, n_nodes, n_tris, &tslot, &n_tslots);
+  // (the slots stay below 3 n_tris: a gap is at most two records per leaf)
+  const bool tris_laid = tri_align && n_tris < (1u << 30) && LayoutTris(nodes, n_nodes, n_tris, &tslot, &n_tslots);
   auto tsl = [&](uint32_t t) { return tris_laid ? tslot[t] : t; };
   for (auto& r : tri_ranges)
     if (r.first < r.second) r = {tsl(r.first), tsl(r.second - 1) + 1};
