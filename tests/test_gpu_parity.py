@@ -278,6 +278,33 @@ def test_triangle_slots(monkeypatch, tmp_path, rubik, env):
         assert (hits == hits_o).all() and bits_equal(t, t_o).all()
 
 
+@pytest.mark.parametrize("case", ["overlap", "shared"])
+def test_triangle_slots_unusual_leaves(case):
+    """LayoutTris on leaf ranges no reference-built tree has: a leaf grown by one triangle into the next
+    leaf's range (partly overlapping ranges: the identity layout is kept) and a leaf given another leaf's
+    range (the same range twice: slotted once).  Both render the oracle's frame."""
+    import dataclasses
+
+    setup = R.make_setup(48, 40, show_model=True, models=[R.synthetic_model(30000, seed=3)])
+    n = setup.scene.nodes.copy()
+    leaves = np.flatnonzero(n["count"] > 0)
+    starts = {int(n["first"][i]): i for i in leaves}
+    i = next(i for i in leaves if int(n["first"][i] + n["count"][i]) in starts)
+    if case == "overlap":
+        n["count"][i] += 1
+    else:
+        j = starts[int(n["first"][i] + n["count"][i])]
+        n["first"][j], n["count"][j] = n["first"][i], n["count"][i]
+    mod = dataclasses.replace(setup, scene=dataclasses.replace(setup.scene, nodes=n))
+    r = R.Renderer(mod)
+    try:
+        slots = r.compute.GetInt("scene.tri_slots")
+    finally:
+        r.close()
+    assert slots == 30000 if case == "overlap" else slots > 30000
+    assert_parity(mod, 2)
+
+
 def test_global_schedule_chosen_by_scene_size():
     """srt_upload_scene's choices for the timed global-scene instance, as bench.py reports them: the torus
     knot (20 MB of nodes + triangles) takes fused sub-steps at 5 waves per SIMD, a 1 M soup (101 MB)
