@@ -7,9 +7,18 @@ the default workload is the same frame shape and sampling on the reference's
 shipped model scene (Rubik.obj, model camera, the 6 lights of src/main.cpp:584-589).
 
 A step = one full progressive render of the workload: the reset frame + `spp`
-sampled frames (one fused kernel launch) and, for N > 1, the gather of every
-rank's row bands to rank 0 (RCCL over xGMI) plus the root-side assembly of the
-frame.  Inputs (scene, noise buffers, lights) are resident in HBM before timing.
+sampled frames (one fused kernel launch per GPU) and, for N > 1, the gather of
+every rank's sRGB8 row bands (4 B/px) to GPU 0 (RCCL over xGMI) plus GPU 0's
+de-interleave of the frame.  Inputs (scene, noise buffers, lights) are resident
+in HBM before timing.
+
+N > 1 runs two ways, with the same kernels and the same exchange:
+  python bench.py --gpus N     the in-process device group (srt_group_*: one context per GPU
+                               in this process, ncclCommInitAll + ncclGather), what a C++ host
+                               embedding the library does; --same-device puts every context on
+                               GPU 0 (device copies instead of RCCL: the one-GPU test);
+  torchrun --nproc-per-node N bench.py --gpus N
+                               one process per GPU, torch.distributed over RCCL.
 
 Two more legs time the real-mesh path (scenes too large for the LDS scene copy,
 traversed from HBM/L2), each under "legs" with its own roofline; `value` is the
@@ -20,7 +29,7 @@ main leg:
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
-       (tests: --backend gloo --same-device runs N ranks on one GPU, staging through the host)
+       (tests: under torchrun, --backend gloo --same-device runs N ranks on one GPU, staging through the host)
 """
 from __future__ import annotations
 
@@ -227,8 +236,11 @@ def build_setup(scene: str, W: int, H: int, spp: int, max_depth: int, synthetic_
 
 
 class RankRun:
-    """One rank's share of a workload: its row bands (srt_set_tiling), its images in torch tensors, and
-    bench's step (clear + one fused launch of `spp` frames + the gather / assembly on N > 1)."""
+    """One rank's share of a workload under torch.distributed (one process per GPU): its row bands
+    (srt_set_tiling), its images in torch tensors, and bench's step (clear + one fused launch of `spp`
+    frames that also encodes the rank's own sRGB8 rows, then on N > 1 the per-frame exchange: one gather
+    of every rank's sRGB8 rows, 4 B/px, into rank 0's preallocated receive buffer, and rank 0's
+    de-interleave).  The radiance stays on its rank; frame() gathers it for a dump."""
 
     def __init__(self, setup, spp, *, rank, world, device, band_rows, stream):
         import torch
@@ -246,10 +258,10 @@ class RankRun:
         self.accum_local = torch.zeros((self.rows_pad, W, 4), dtype=torch.float32, device=self.dev)
         self.out_local = torch.zeros((self.rows_pad, W), dtype=torch.int32, device=self.dev)
         self.c.set_image_buffers(self.accum_local.data_ptr(), self.out_local.data_ptr())
-        self.full_accum = self.full_out = None
+        self.recv_out = self.full_out = None
         if rank == 0 and world > 1:
-            self.full_accum = torch.empty((H, W, 4), dtype=torch.float32, device=self.dev)
-            self.full_out = torch.empty((H, W), dtype=torch.int32, device=self.dev)
+            self.recv_out = torch.empty((world, self.rows_pad, W), dtype=torch.int32, device=self.dev)
+            self.full_out = torch.zeros((H, W), dtype=torch.int32, device=self.dev)
 
     def count(self) -> dict:
         """Deterministic counting run (untimed): the work every step repeats."""
@@ -263,70 +275,150 @@ class RankRun:
         from srt_amd import parallel as PAR
 
         self.rdr.clear()
-        self.c.render_frames(2, self.spp, write_output=(self.world == 1), count=False)
+        self.c.render_frames(2, self.spp, write_output=True, count=False)
         self.rdr.accum_frames = self.spp + 1
-        if self.world > 1:  # the one exchange: every rank's radiance rows to rank 0 (RCCL over xGMI)
-            stacked = PAR.gather_bands(self.accum_local, dst=0)
+        if self.world > 1:  # the one exchange: every rank's sRGB8 rows to rank 0 (RCCL over xGMI)
+            PAR.gather_bands(self.out_local, dst=0, out=self.recv_out)
             if self.rank == 0:
-                self.c.assemble_bands(stacked.data_ptr(), self.world, self.rows_pad, self.band, self.spp + 1,
-                                      self.full_accum.data_ptr(), self.full_out.data_ptr())
+                self.c.assemble_output_bands(self.recv_out.data_ptr(), self.world, self.rows_pad, self.band,
+                                             self.full_out.data_ptr())
 
-    def frame(self):
-        """Rank 0's frame after a step: (accum (H, W, 4) float32, sRGB8 (H, W, 4) uint8) on the host."""
+    def sync(self):
         import torch
 
         torch.cuda.synchronize(self.dev)
+
+    def kernel_ms(self) -> list:
+        return [self.c.last_kernel_ms()]  # HIP events around sample_kernel on the launch stream
+
+    def frame(self):
+        """Rank 0's frame after a step: (accum (H, W, 4) float32, sRGB8 (H, W, 4) uint8) on the host; None
+        on other ranks.  Collective for N > 1 (every rank calls it): the radiance rows are gathered here."""
+        import torch
+
+        from srt_amd import parallel as PAR
+
+        torch.cuda.synchronize(self.dev)
+        H, W = self.setup.height, self.setup.width
         if self.world > 1:
-            acc, out = self.full_accum, self.full_out
+            stacked = PAR.gather_bands(self.accum_local, dst=0)
+            if self.rank != 0:
+                return None
+            acc = torch.empty((H, W, 4), dtype=torch.float32, device=self.dev)
+            self.c.assemble_bands(stacked.data_ptr(), self.world, self.rows_pad, self.band, self.spp + 1,
+                                  acc.data_ptr(), None)
+            out = self.full_out
         else:
             acc, out = self.accum_local, self.out_local
-        H, W = self.setup.height, self.setup.width
+        torch.cuda.synchronize(self.dev)
         return (acc[:H].cpu().numpy(), out[:H].cpu().numpy().view(np.uint8).reshape(H, W, 4))
 
     def close(self):
         self.rdr.close()
 
 
-def run_leg(setup, spp, args, *, rank, world, device, stream):
+class GroupRun:
+    """The whole workload tiled over N devices of this one process through the C ABI's device group
+    (srt_group_*, the C++ host's multi-GPU path): one context and stream per device, each rendering its
+    row bands and encoding its own sRGB8 rows; per frame one gather of those rows (ncclGather over xGMI,
+    communicators from ncclCommInitAll; device copies when a device repeats, as under --same-device) to
+    device 0, which de-interleaves them.  No torch.distributed and no rank processes: this is what
+    `python bench.py --gpus N` runs when it is not launched under torch.distributed.run."""
+
+    def __init__(self, setup, spp, *, devices, band_rows):
+        from srt_amd import render as R
+
+        self.setup, self.spp = setup, spp
+        self.devices = list(devices)
+        self.grp = R.GroupRenderer(setup, self.devices, band_rows=band_rows)
+
+    def count(self) -> dict:
+        return self.grp.count(self.spp)
+
+    def step(self):
+        self.grp.render(self.spp)
+
+    def sync(self):
+        self.grp.finish()
+
+    def kernel_ms(self) -> list:
+        return self.grp.kernel_ms()
+
+    def frame(self):
+        return self.grp.accum(), self.grp.output()
+
+    def info(self) -> dict:
+        g = self.grp
+        return {"mode": "in-process device group (srt_group_*)", "transport": g.transport,
+                "rccl_ranks": g.get_int("ranks"), "contexts": g.get_int("contexts"), "devices": self.devices,
+                "gather_bytes_per_frame": g.get_int("bytes.output") * 1024,
+                "radiance_gathers_in_timed_steps": g.get_int("gathers.accum")}
+
+    def close(self):
+        self.grp.close()
+
+
+def run_leg(setup, spp, args, *, mode, rank, world, device, stream):
     """Counting run, warmup, then exactly `steps` timed steps bracketed by barrier + synchronize;
-    returns (elapsed max over ranks, total rays over ranks, this rank's stats, kernel ms list, run)."""
+    returns (elapsed max over ranks, total rays over ranks, this rank's stats, per-context kernel ms lists,
+    run)."""
     import torch
     import torch.distributed as dist
 
-    run = RankRun(setup, spp, rank=rank, world=world, device=device, band_rows=args.band_rows, stream=stream)
+    if mode == "group":
+        run = GroupRun(setup, spp, devices=[0] * args.gpus if args.same_device else range(args.gpus),
+                       band_rows=args.band_rows)
+    else:
+        run = RankRun(setup, spp, rank=rank, world=world, device=device, band_rows=args.band_rows, stream=stream)
     st = run.count()
     counts = torch.tensor([float(st["rays"])], dtype=torch.float64)
-    if world > 1:
+    if mode == "dist" and world > 1:
         counts = counts.to(run.dev) if args.backend == "nccl" else counts
         dist.all_reduce(counts)
     total_rays = float(counts[0].item())
     for _ in range(args.warmup):
         run.step()
-    torch.cuda.synchronize(run.dev)
-    if world > 1:
+    run.sync()
+    if mode == "dist" and world > 1:
         dist.barrier()
-    torch.cuda.synchronize(run.dev)
+    run.sync()
     kernel_ms = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run.step()
-        torch.cuda.synchronize(run.dev)
-        kernel_ms.append(run.c.last_kernel_ms())  # HIP events around sample_kernel on the launch stream
-    torch.cuda.synchronize(run.dev)
-    if world > 1:
+        run.sync()
+        kernel_ms.append(run.kernel_ms())
+    run.sync()
+    if mode == "dist" and world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64)
-    if world > 1:
+    if mode == "dist" and world > 1:
         elapsed = elapsed.to(run.dev) if args.backend == "nccl" else elapsed
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    return float(elapsed.item()), total_rays, st, kernel_ms, run
+    per_ctx = [list(x) for x in zip(*kernel_ms)]  # [context][step]
+    return float(elapsed.item()), total_rays, st, per_ctx, run
+
+
+def ranks_kernel_ms(per_ctx, args, mode, world, dev):
+    """Mean sample-kernel ms of every rank (context), rank order; under torch.distributed one all_gather."""
+    import torch
+    import torch.distributed as dist
+
+    mine = [float(np.mean(x)) for x in per_ctx]
+    if mode != "dist" or world == 1:
+        return [round(v, 3) for v in mine]
+    t = torch.tensor(mine, dtype=torch.float64)
+    t = t.to(dev) if args.backend == "nccl" else t
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [round(float(v), 3) for p in parts for v in p.cpu().tolist()]
 
 
 KERNEL_LDS = "srt::sample_kernel<false, true, true, 1024, false, false, 4> (LDS-resident scene)"
 
 
-def timed_kernel(run, scene: str) -> str:
+def timed_kernel(c, scene: str) -> str:
     """The sample_kernel instance the run's timed launches took.  Global-scene mode: fused sub-steps for
     trees under 600 MB (both legs), the IL pattern past it (C5); the fused instance at 5 waves per SIMD
     for trees under 48 MB (the surface-mesh leg), else 4 (srt_get_int's scene.* names)."""
@@ -334,10 +426,24 @@ def timed_kernel(run, scene: str) -> str:
         return KERNEL_LDS
     if scene == "spheres":
         return "srt::sphere_kernel<false> (spheres: no BVH, 3 waves per SIMD)"
-    fused = run.c.GetInt("scene.fused") == 1
-    gw = run.c.GetInt("scene.global_waves") if fused else 4
+    fused = c.GetInt("scene.fused") == 1
+    gw = c.GetInt("scene.global_waves") if fused else 4
     return (f"srt::sample_kernel<false, false, true, 256, false, {'true' if fused else 'false'}, {gw}> "
             f"(global-scene mode, {'fused' if fused else 'IL'} sub-steps, {gw} waves per SIMD)")
+
+
+def run_compute(run):
+    return run.grp.parts[0].compute if isinstance(run, GroupRun) else run.c
+
+
+def parallelism(args, mode, world, run) -> str:
+    if world == 1:
+        return "single GPU"
+    if mode == "group":
+        return (f"row-band tiling x{world} ({args.band_rows}-row bands) over the devices of one process + per-frame "
+                f"sRGB8 gather to device 0 ({'RCCL ncclGather' if run.grp.transport == 'rccl' else 'device copies'})")
+    return (f"row-band tiling x{world} ({args.band_rows}-row bands), one process per GPU + per-frame sRGB8 gather "
+            f"to rank 0 ({'RCCL' if args.backend == 'nccl' else 'gloo'})")
 
 
 def main(argv=None):
@@ -345,72 +451,76 @@ def main(argv=None):
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world == 1 and args.gpus > 1:
-        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    if world_env > 1:
+        if world_env != args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} differs from WORLD_SIZE {world_env}")
+        mode, world = "dist", world_env  # torch.distributed.run: one rank per GPU
+    elif args.gpus > 1:
+        mode, world = "group", args.gpus  # plain `python bench.py --gpus N`: the in-process device group
+        if not args.same_device and torch.cuda.device_count() < args.gpus:
+            raise SystemExit(f"--gpus {args.gpus}: only {torch.cuda.device_count()} devices visible")
+    else:
+        mode, world = "single", 1
     device = 0 if args.same_device else local_rank
     torch.cuda.set_device(device)
-    if world > 1:
+    if mode == "dist":
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group("gloo")
+    dev = torch.device("cuda", device)
 
     W, H, spp = args.width, args.height, args.spp
     setup, wl_name = build_setup(args.scene, W, H, spp, args.max_depth, args.synthetic_tris)
-    dev = torch.device("cuda", device)
     stream = torch.cuda.Stream(device=dev)   # a real (non-null) stream shared by torch and the library
     torch.cuda.set_stream(stream)
 
-    elapsed_s, total_rays, st, kernel_ms, run = run_leg(setup, spp, args, rank=rank, world=world, device=device,
-                                                        stream=stream)
-    if args.dump and rank == 0:
-        acc, out = run.frame()
-        np.savez(args.dump, accum=acc, out=out)
-    kname = timed_kernel(run, args.scene)
+    elapsed_s, total_rays, st, kernel_ms, run = run_leg(setup, spp, args, mode=mode, rank=rank, world=world,
+                                                        device=device, stream=stream)
+    group_info = run.info() if mode == "group" else None  # (before a dump's radiance gather)
+    if args.dump:
+        fr = run.frame()
+        if rank == 0:
+            np.savez(args.dump, accum=fr[0], out=fr[1])
+    kname = timed_kernel(run_compute(run), args.scene)
+    par = parallelism(args, mode, world, run)
+    rk_ms = ranks_kernel_ms(kernel_ms, args, mode, world, dev)
     run.close()
 
     legs = []
-    if not args.no_global_leg:
-        gsetup, gname = build_setup("synthetic", 1920, 1080, args.global_spp, 5, args.global_tris)
-        g_el, g_rays, g_st, g_kms, g_run = run_leg(gsetup, args.global_spp, args, rank=rank, world=world,
+    for leg, enabled, scene, lw, lh, lspp, ntri in (
+            ("global_scene", not args.no_global_leg, "synthetic", 1920, 1080, args.global_spp, args.global_tris),
+            ("surface_mesh", not args.no_surface_leg, "torusknot", 1920, 1080, args.surface_spp, 0)):
+        if not enabled:
+            continue
+        lsetup, lname = build_setup(scene, lw, lh, lspp, 5, ntri)
+        l_el, l_rays, l_st, l_kms, l_run = run_leg(lsetup, lspp, args, mode=mode, rank=rank, world=world,
                                                    device=device, stream=stream)
-        g_kname = timed_kernel(g_run, "synthetic")
-        g_run.close()
+        l_kname = timed_kernel(run_compute(l_run), scene)
+        l_rk = ranks_kernel_ms(l_kms, args, mode, world, dev)
+        l_run.close()
         if rank == 0:
-            g_k = float(np.mean(g_kms))
+            desc = (f"synthetic {ntri} triangles (SURVEY 8d generator)" if scene == "synthetic" else
+                    "torus-knot tube, 262144 triangles (closed surface mesh; srt_amd.render.torus_knot_triangles), "
+                    "model camera and lights")
             legs.append({
-                "leg": "global_scene", "workload": gname, "value": round(g_rays * args.steps / g_el / 1e6, 3),
-                "unit": "Mrays/s", "ms_per_step": round(g_el * 1e3 / args.steps, 3),
-                "config": {"scene": f"synthetic {args.global_tris} triangles (SURVEY 8d generator)", "width": 1920,
-                           "height": 1080, "spp": args.global_spp, "max_depth": 5},
-                "roofline": roofline(gname, g_k, algorithmic_bytes(g_st) if world == 1 else 0, g_kname,
-                                     global_mode=True),
-            })
-
-    if not args.no_surface_leg:
-        ssetup, sname = build_setup("torusknot", 1920, 1080, args.surface_spp, 5, 0)
-        s_el, s_rays, s_st, s_kms, s_run = run_leg(ssetup, args.surface_spp, args, rank=rank, world=world,
-                                                   device=device, stream=stream)
-        s_kname = timed_kernel(s_run, "torusknot")
-        s_run.close()
-        if rank == 0:
-            legs.append({
-                "leg": "surface_mesh", "workload": sname, "value": round(s_rays * args.steps / s_el / 1e6, 3),
-                "unit": "Mrays/s", "ms_per_step": round(s_el * 1e3 / args.steps, 3),
-                "config": {"scene": "torus-knot tube, 262144 triangles (closed surface mesh; srt_amd.render."
-                                    "torus_knot_triangles), model camera and lights", "width": 1920, "height": 1080,
-                           "spp": args.surface_spp, "max_depth": 5},
-                "roofline": roofline(sname, float(np.mean(s_kms)), algorithmic_bytes(s_st) if world == 1 else 0,
-                                     s_kname, global_mode=True),
+                "leg": leg, "workload": lname, "value": round(l_rays * args.steps / l_el / 1e6, 3),
+                "unit": "Mrays/s", "ms_per_step": round(l_el * 1e3 / args.steps, 3),
+                "config": {"scene": desc, "width": lw, "height": lh, "spp": lspp, "max_depth": 5},
+                "kernel_ms_per_rank": l_rk,
+                "roofline": roofline(lname, float(np.mean(l_kms[0])), algorithmic_bytes(l_st), l_kname,
+                                     global_mode=True) if world == 1 else
+                {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
+                 "kernel_ms": round(float(np.mean(l_kms[0])), 3), "note": "roofline reported at N=1"},
             })
 
     if rank == 0:
         ms_per_step = elapsed_s * 1e3 / args.steps
         value = total_rays * args.steps / elapsed_s / 1e6
-        k_ms = float(np.mean(kernel_ms))
+        k_ms = float(np.mean(kernel_ms[0]))
         line = {
             "metric": "Mrays/s (CheckHit queries: camera + bounce + shadow rays) at the BASELINE frame/spp",
             "value": round(value, 3),
@@ -428,28 +538,40 @@ def main(argv=None):
                        if args.scene == "rubik" else f"{args.scene} scene"),
             "config": {
                 "workload": wl_name, "width": W, "height": H, "spp": spp, "max_depth": args.max_depth,
-                "scene": args.scene, "lights": int(len(setup.lights)),
-                "parallelism": f"row-band tiling x{world} ({args.band_rows}-row bands) + gather to rank 0 "
-                               f"({'RCCL' if args.backend == 'nccl' else 'gloo'})" if world > 1 else "single GPU",
+                "scene": args.scene, "lights": int(len(setup.lights)), "parallelism": par,
             },
             "frame_ms": round(ms_per_step / spp, 4),
             "msamples_per_s": round(W * H * spp * args.steps / elapsed_s / 1e6, 3),
             "rays_per_step": int(total_rays),
             "code_hash": code_hash(),
-            # per-rank counters describe rank 0's launch: the roofline is a 1-GPU figure
-            "roofline": roofline(wl_name, k_ms, algorithmic_bytes(st), kname, global_mode=args.scene in ("synthetic", "torusknot"))
+            "kernel_ms_per_rank": rk_ms,
+            # per-rank counters describe one launch on one GPU: the roofline is a 1-GPU figure
+            "roofline": roofline(wl_name, k_ms, algorithmic_bytes(st), kname,
+                                 global_mode=args.scene in ("synthetic", "torusknot"))
             if world == 1 else
             {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
              "kernel_ms": round(k_ms, 3), "note": "roofline reported at N=1"},
             "legs": legs,
         }
+        if group_info is not None:
+            line["group"] = group_info
+        elif mode == "dist":
+            line["group"] = {"mode": "torch.distributed, one process per GPU", "backend": args.backend,
+                             "world_size": world,
+                             "gather_bytes_per_frame": world * PAR_rows_pad(H, args.band_rows, world) * W * 4}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(setup, 2, args.cpu_seconds)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if mode == "dist":
         dist.destroy_process_group()
+
+
+def PAR_rows_pad(height, band_rows, world):
+    from srt_amd import parallel as PAR
+
+    return PAR.rows_pad(height, band_rows, world)
 
 
 if __name__ == "__main__":

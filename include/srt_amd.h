@@ -150,15 +150,26 @@ int srt_get_int(srt_context* ctx, const char* name, int* v);
  * The reference's frame loop (src/main.cpp:657-725) drives one GL context.  A C++ embedder tiles the
  * same frame over the GPUs of a node with a group of contexts, one per device, each holding the scene,
  * noise and lights (srt_upload_scene etc. on every context): context i renders the row bands b of
- * `band_rows` rows with b % n == i, with global pixel coordinates; one gather of every context's
- * radiance rows to context 0 -- ncclGather over xGMI (RCCL, one communicator per device from
- * ncclCommInitAll) -- then context 0 de-interleaves the bands and encodes sRGB8 (srt_assemble_bands).
+ * `band_rows` rows with b % n == i, with global pixel coordinates, and encodes its own rows' sRGB8
+ * (accumFrames is one uniform for all).  Per frame, one gather moves every context's sRGB8 rows
+ * (4 B/px) to context 0 -- ncclGather over xGMI (RCCL, one communicator per device from
+ * ncclCommInitAll, librccl loaded at srt_group_create) on a gather stream of its own per device,
+ * double-buffered so frame k's gather overlaps frame k+1's render -- and context 0 de-interleaves
+ * the bands.  The radiance (RGBA32F) stays distributed: it is gathered only when the full
+ * accumulation image is asked for (srt_group_read_accum, srt_group_image_pointers' accum_dev).
  * The frame is bit-identical to one device's.  A device list that repeats a device (RCCL takes one rank
  * per device), or SRT_GROUP_TRANSPORT=copy, gathers with device-to-device copies instead.
- * Contexts stay owned by the caller and must outlive the group. */
+ * Contexts stay owned by the caller and must outlive the group; srt_group_destroy gives each back
+ * its own full-frame images (tiling rank 0 of 1), so they can be dispatched again. */
 typedef struct srt_group srt_group;
 int srt_group_create(srt_context* const* ctxs, int n, int band_rows, srt_group** out);
 int srt_group_destroy(srt_group* g);
+/* "contexts"; "ranks" (ncclCommCount of the communicators, or the contexts under the copy
+ * transport); "gathers.output" / "gathers.accum" (gathers issued so far); "bytes.output" /
+ * "bytes.accum" (bytes one such gather moves into context 0, in KiB). */
+int srt_group_get_int(srt_group* g, const char* name, int* v);
+/* Each context's srt_last_kernel_ms (HIP events around its sample_kernel launches), n entries. */
+int srt_group_last_kernel_ms(srt_group* g, float* ms, int n);
 /* Uniform setters broadcast to every context (the names of srt_set_*). */
 int srt_group_set_bool(srt_group* g, const char* name, int v);
 int srt_group_set_int(srt_group* g, const char* name, int v);
@@ -167,13 +178,15 @@ int srt_group_set_vec3(srt_group* g, const char* name, float x, float y, float z
 /* After Width/Height: tiles the contexts (srt_set_tiling i of n), gives each an equal-size padded band
  * image (the gather's send buffer) and context 0 the full-frame images. */
 int srt_group_alloc_images(srt_group* g);
-/* glDispatchCompute on every context (srt_dispatch), then the gather and the full-frame assembly
- * (image0 written unless resetAccumBuffer, as the reference's reset dispatch returns before its store). */
+/* glDispatchCompute on every context (srt_dispatch), then the sRGB8 gather and the full-frame image0
+ * (not for a resetAccumBuffer dispatch, as the reference's reset dispatch returns before its store;
+ * pixels outside the dispatch extent keep their values). */
 int srt_group_dispatch(srt_group* g, uint32_t groups_x, uint32_t groups_y);
-/* srt_render_frames on every context, then the gather and the assembly for the last frame. */
+/* srt_render_frames on every context, then the sRGB8 gather and the image0 of the last frame. */
 int srt_group_render_frames(srt_group* g, int frame_first, int nframes);
-int srt_group_finish(srt_group* g);  /* glFinish on every device */
-/* The full frame (Width x Height) on the host, or its device pointers on context 0's device. */
+int srt_group_finish(srt_group* g);  /* glFinish on every device (render and gather streams) */
+/* The full frame (Width x Height) on the host, or its device pointers on context 0's device (asking
+ * for accum_dev enqueues the radiance gather; read after srt_group_finish). */
 int srt_group_read_accum(srt_group* g, float* host_rgba32f, size_t bytes);
 int srt_group_read_output(srt_group* g, uint8_t* host_rgba8, size_t bytes);
 int srt_group_image_pointers(srt_group* g, void** accum_dev, void** out_dev);
@@ -248,6 +261,11 @@ int srt_set_image_buffers(srt_context* ctx, void* accum_dev, void* out_dev);
  * NULL).  Enqueued on the context's stream. */
 int srt_assemble_bands(srt_context* ctx, const void* gathered, int nranks, int rows_pad, int band_rows, int frames,
                        void* accum_full, void* out_full);
+/* The per-frame form: every rank encoded its own rows' sRGB8 (image0; accumFrames is one uniform
+ * for all ranks), `gathered_rgba8` holds nranks blocks of rows_pad packed RGBA8 rows, and only the
+ * full-frame image0 is written -- 4 B per pixel cross the interconnect instead of 16. */
+int srt_assemble_output_bands(srt_context* ctx, const void* gathered_rgba8, int nranks, int rows_pad, int band_rows,
+                              void* out_full);
 
 /* Closest-hit query: the test kernel ray_intersects.glsl:135-161 fed through
  * AssetUtils::UpdateRays (gpu_loader.cpp:198-210); hits[i] = triangle index

@@ -1,11 +1,21 @@
 // group.cpp -- the multi-GPU frame of one host process (include/srt_amd.h, srt_group_*).
 //
 // The reference renders one frame per glDispatchCompute on one GL context (src/main.cpp:657-725).
-// Here n contexts, one per device, render interleaved row bands of the same frame (srt_set_tiling),
-// and the only exchange is one gather of every context's radiance rows to context 0: ncclGather
-// over xGMI (RCCL) when the devices are distinct, device-to-device copies when a device repeats
-// (RCCL takes one rank per device; this lets one GPU run the group's whole path for tests).
-// Context 0 then de-interleaves the bands and writes the sRGB8 image (srt_assemble_bands).
+// Here n contexts, one per device, render interleaved row bands of the same frame (srt_set_tiling)
+// and each encodes its own rows' sRGB8 (accumFrames is one uniform for all).  Per frame, the only
+// exchange is one gather of those 4-B pixels to context 0: ncclGather over xGMI (RCCL) when the
+// devices are distinct, device-to-device copies when a device repeats (RCCL takes one rank per
+// device; this lets one GPU run the group's whole path for tests).  Context 0 then de-interleaves
+// the bands.  The radiance (16 B/px) stays where it was rendered -- the next frame adds to it there
+// -- and is gathered only when the full accumulation image is asked for.
+//
+// Streams.  A context renders on its own stream; each device also has a gather stream, so frame
+// k's gather and assembly run beside frame k+1's render.  The sRGB8 band images are
+// double-buffered for that: frame k writes buffer k % 2, and a render waits (hipStreamWaitEvent)
+// for the gather that last read the buffer it is about to write, and for the last radiance
+// gather.  Under the copy transport a context's copy into context 0's receive buffer waits for
+// the previous assembly, which read that buffer.
+#include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
@@ -18,17 +28,74 @@
 
 #include "srt_internal.hpp"
 
+namespace {
+
+// RCCL, loaded when the first group that needs it is created: the library itself does not depend on
+// it, so an embedder that never tiles a frame over devices needs no librccl.  (When PyTorch has
+// loaded its own librccl.so.1 first, dlopen returns that one: both carry the soname.)
+struct Rccl {
+  bool ok = false;
+  std::string err;
+  decltype(&ncclCommInitAll) CommInitAll = nullptr;
+  decltype(&ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&ncclCommCount) CommCount = nullptr;
+  decltype(&ncclGather) Gather = nullptr;
+  decltype(&ncclGroupStart) GroupStart = nullptr;
+  decltype(&ncclGroupEnd) GroupEnd = nullptr;
+  decltype(&ncclGetErrorString) GetErrorString = nullptr;
+};
+
+const Rccl& rccl() {
+  static const Rccl r = [] {
+    Rccl x;
+    void* h = nullptr;
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+      if ((h = dlopen(name, RTLD_NOW | RTLD_GLOBAL)) != nullptr) break;
+    if (!h) {
+      const char* e = dlerror();
+      x.err = std::string("cannot load librccl.so.1: ") + (e ? e : "");
+      return x;
+    }
+    auto sym = [&](auto* fn, const char* name) {
+      *fn = reinterpret_cast<std::remove_pointer_t<decltype(fn)>>(dlsym(h, name));
+      if (!*fn && x.err.empty()) x.err = std::string("librccl: no symbol ") + name;
+    };
+    sym(&x.CommInitAll, "ncclCommInitAll");
+    sym(&x.CommDestroy, "ncclCommDestroy");
+    sym(&x.CommCount, "ncclCommCount");
+    sym(&x.Gather, "ncclGather");
+    sym(&x.GroupStart, "ncclGroupStart");
+    sym(&x.GroupEnd, "ncclGroupEnd");
+    sym(&x.GetErrorString, "ncclGetErrorString");
+    x.ok = x.err.empty();
+    return x;
+  }();
+  return r;
+}
+
+}  // namespace
+
 struct srt_group {
   std::vector<srt_context*> ctx;
   std::vector<int> dev;
-  std::vector<hipStream_t> stream;
-  std::vector<ncclComm_t> comm;  // empty: copy transport
-  std::vector<hipEvent_t> done;  // per context: its bands are rendered (copy transport)
+  std::vector<hipStream_t> stream;  // each context's render stream (srt_stream)
+  std::vector<hipStream_t> xfer;    // per context: its gather stream (on its device)
+  std::vector<ncclComm_t> comm;     // empty: copy transport
+  std::vector<hipEvent_t> rendered;  // per context: its launches so far (render stream)
+  std::vector<hipEvent_t> sent[2];   // per context and sRGB8 buffer: the gather that read it (gather stream)
+  std::vector<hipEvent_t> acc_sent;  // per context: the radiance gather that read its accumulation image
+  std::vector<hipEvent_t> arrived;   // per context, copy transport: its rows are in context 0's buffer
+  hipEvent_t assembled = nullptr;    // context 0's gather stream: the last assembly (it read recv_*)
   int band_rows = 8;
   int W = 0, H = 0, rows_pad = 0;
-  std::vector<void*> band_accum, band_out;  // per context, rows_pad rows (the gather's send buffers)
-  void* recv = nullptr;                      // context 0: n * rows_pad rows
-  void* full_accum = nullptr;                // context 0: the assembled frame
+  int cur = 0;               // the sRGB8 buffer the next frame writes
+  bool accum_stale = false;  // full_accum is older than the contexts' radiance
+  long long gathers_out = 0, gathers_acc = 0;
+  std::vector<void*> band_accum;  // per context, rows_pad rows RGBA32F (its accumulation image)
+  std::vector<void*> band_out[2];  // per context, rows_pad rows RGBA8 (its image0, double-buffered)
+  void* recv_out = nullptr;        // context 0: n * rows_pad rows RGBA8
+  void* recv_acc = nullptr;        // context 0: n * rows_pad rows RGBA32F (allocated on first use)
+  void* full_accum = nullptr;      // context 0: the assembled frame
   void* full_out = nullptr;
 };
 
@@ -42,57 +109,155 @@ namespace {
       return SRT_ERR_HIP;                                                     \
     }                                                                         \
   } while (0)
-#define GNCCL(x)                                                                \
-  do {                                                                          \
-    ncclResult_t r_ = (x);                                                      \
-    if (r_ != ncclSuccess) {                                                    \
-      srt::SetError(std::string("group: " #x ": ") + ncclGetErrorString(r_)); \
-      return SRT_ERR_HIP;                                                       \
-    }                                                                           \
+#define GNCCL(x)                                                                        \
+  do {                                                                                  \
+    ncclResult_t r_ = (x);                                                              \
+    if (r_ != ncclSuccess) {                                                            \
+      srt::SetError(std::string("group: " #x ": ") + rccl().GetErrorString(r_));      \
+      return SRT_ERR_HIP;                                                               \
+    }                                                                                   \
   } while (0)
 
 void FreeImages(srt_group* g) {
   for (size_t i = 0; i < g->ctx.size(); ++i) {
     (void)hipSetDevice(g->dev[i]);
     if (i < g->band_accum.size() && g->band_accum[i]) (void)hipFree(g->band_accum[i]);
-    if (i < g->band_out.size() && g->band_out[i]) (void)hipFree(g->band_out[i]);
+    for (auto& bo : g->band_out)
+      if (i < bo.size() && bo[i]) (void)hipFree(bo[i]);
   }
   g->band_accum.clear();
-  g->band_out.clear();
+  for (auto& bo : g->band_out) bo.clear();
   if (!g->dev.empty()) (void)hipSetDevice(g->dev[0]);
-  for (void* p : {g->recv, g->full_accum, g->full_out})
+  for (void* p : {g->recv_out, g->recv_acc, g->full_accum, g->full_out})
     if (p) (void)hipFree(p);
-  g->recv = g->full_accum = g->full_out = nullptr;
+  g->recv_out = g->recv_acc = g->full_accum = g->full_out = nullptr;
 }
 
-// The gather of every context's band rows into context 0's receive buffer, then the assembly of the
-// full frame for accumFrames = `frames` (sRGB8 image too when write_out).
-int GatherAssemble(srt_group* g, int frames, bool write_out) {
-  const size_t floats = (size_t)g->rows_pad * g->W * 4;
+void DestroyStreamsEvents(srt_group* g) {
+  auto destroy = [&](std::vector<hipEvent_t>& v) {
+    for (size_t i = 0; i < v.size(); ++i) {
+      if (!v[i]) continue;
+      (void)hipSetDevice(g->dev[i]);
+      (void)hipEventDestroy(v[i]);
+    }
+    v.clear();
+  };
+  destroy(g->rendered);
+  destroy(g->sent[0]);
+  destroy(g->sent[1]);
+  destroy(g->acc_sent);
+  destroy(g->arrived);
+  if (g->assembled) {
+    (void)hipSetDevice(g->dev[0]);
+    (void)hipEventDestroy(g->assembled);
+    g->assembled = nullptr;
+  }
+  for (size_t i = 0; i < g->xfer.size(); ++i) {
+    if (!g->xfer[i]) continue;
+    (void)hipSetDevice(g->dev[i]);
+    (void)hipStreamDestroy(g->xfer[i]);
+  }
+  g->xfer.clear();
+}
+
+int CreateStreamsEvents(srt_group* g) {
   const int n = (int)g->ctx.size();
-  if (!g->comm.empty()) {
-    GNCCL(ncclGroupStart());
-    for (int i = 0; i < n; ++i) {
-      GHIP(hipSetDevice(g->dev[i]));
-      GNCCL(ncclGather(g->band_accum[i], i == 0 ? g->recv : nullptr, floats, ncclFloat32, 0, g->comm[i],
-                       g->stream[i]));
-    }
-    GNCCL(ncclGroupEnd());
-  } else {
-    for (int i = 0; i < n; ++i) {
-      GHIP(hipSetDevice(g->dev[i]));
-      GHIP(hipEventRecord(g->done[i], g->stream[i]));
-    }
-    GHIP(hipSetDevice(g->dev[0]));
-    for (int i = 0; i < n; ++i) {
-      GHIP(hipStreamWaitEvent(g->stream[0], g->done[i], 0));
-      char* dst = static_cast<char*>(g->recv) + (size_t)i * floats * sizeof(float);
-      GHIP(hipMemcpyPeerAsync(dst, g->dev[0], g->band_accum[i], g->dev[i], floats * sizeof(float), g->stream[0]));
+  g->xfer.assign(n, nullptr);
+  for (auto* v : {&g->rendered, &g->sent[0], &g->sent[1], &g->acc_sent, &g->arrived}) v->assign(n, nullptr);
+  for (int i = 0; i < n; ++i) {
+    GHIP(hipSetDevice(g->dev[i]));
+    GHIP(hipStreamCreateWithFlags(&g->xfer[i], hipStreamNonBlocking));
+    for (auto* v : {&g->rendered, &g->sent[0], &g->sent[1], &g->acc_sent, &g->arrived}) {
+      GHIP(hipEventCreateWithFlags(&(*v)[i], hipEventDisableTiming));
+      GHIP(hipEventRecord((*v)[i], g->xfer[i]));  // recorded once: every wait below has a completed event
     }
   }
   GHIP(hipSetDevice(g->dev[0]));
-  return srt_assemble_bands(g->ctx[0], g->recv, n, g->rows_pad, g->band_rows, std::max(frames, 1), g->full_accum,
-                            write_out ? g->full_out : nullptr);
+  GHIP(hipEventCreateWithFlags(&g->assembled, hipEventDisableTiming));
+  GHIP(hipEventRecord(g->assembled, g->xfer[0]));
+  return SRT_OK;
+}
+
+// Before a launch that writes sRGB8 buffer `b`: every context's image buffers point at its band
+// images, and its render stream waits for the gathers that last read them.
+int PrepareLaunch(srt_group* g, int b) {
+  for (size_t i = 0; i < g->ctx.size(); ++i) {
+    if (int rc = srt_set_image_buffers(g->ctx[i], g->band_accum[i], g->band_out[b][i])) return rc;
+    GHIP(hipSetDevice(g->dev[i]));
+    GHIP(hipStreamWaitEvent(g->stream[i], g->sent[b][i], 0));
+    GHIP(hipStreamWaitEvent(g->stream[i], g->acc_sent[i], 0));
+  }
+  return SRT_OK;
+}
+
+// One gather of every context's `bytes` at send[i] into context 0's `recv` (rank order), on the
+// gather streams, behind each context's launches so far; `sent_ev[i]` marks the end of context i's
+// part (its send buffer may be written again after it).
+int Gather(srt_group* g, const std::vector<void*>& send, void* recv, size_t bytes, std::vector<hipEvent_t>& sent_ev) {
+  const int n = (int)g->ctx.size();
+  for (int i = 0; i < n; ++i) {
+    GHIP(hipSetDevice(g->dev[i]));
+    GHIP(hipEventRecord(g->rendered[i], g->stream[i]));
+    GHIP(hipStreamWaitEvent(g->xfer[i], g->rendered[i], 0));
+  }
+  if (!g->comm.empty()) {
+    const Rccl& R = rccl();
+    GNCCL(R.GroupStart());
+    for (int i = 0; i < n; ++i) {
+      GHIP(hipSetDevice(g->dev[i]));
+      GNCCL(R.Gather(send[i], i == 0 ? recv : nullptr, bytes, ncclUint8, 0, g->comm[i], g->xfer[i]));
+    }
+    GNCCL(R.GroupEnd());
+  } else {
+    for (int i = 0; i < n; ++i) {
+      GHIP(hipSetDevice(g->dev[i]));
+      // context 0's buffer is free once the last assembly (on context 0's gather stream) has read it
+      if (i > 0) GHIP(hipStreamWaitEvent(g->xfer[i], g->assembled, 0));
+      char* dst = static_cast<char*>(recv) + (size_t)i * bytes;
+      GHIP(hipMemcpyPeerAsync(dst, g->dev[0], send[i], g->dev[i], bytes, g->xfer[i]));
+      GHIP(hipEventRecord(g->arrived[i], g->xfer[i]));
+    }
+    GHIP(hipSetDevice(g->dev[0]));
+    for (int i = 1; i < n; ++i) GHIP(hipStreamWaitEvent(g->xfer[0], g->arrived[i], 0));
+  }
+  for (int i = 0; i < n; ++i) {
+    GHIP(hipSetDevice(g->dev[i]));
+    GHIP(hipEventRecord(sent_ev[i], g->xfer[i]));
+  }
+  GHIP(hipSetDevice(g->dev[0]));
+  return SRT_OK;
+}
+
+// Frame's end: the sRGB8 rows of buffer `b` to context 0, de-interleaved into full_out over the
+// dispatch extent.
+int GatherOutput(srt_group* g, int b, int ext_w, int ext_h) {
+  const size_t bytes = (size_t)g->rows_pad * g->W * 4;
+  if (int rc = Gather(g, g->band_out[b], g->recv_out, bytes, g->sent[b])) return rc;
+  if (int rc = srt::AssembleOutputOn(g->ctx[0], g->xfer[0], g->recv_out, (int)g->ctx.size(), g->rows_pad,
+                                     g->band_rows, ext_w, ext_h, g->full_out))
+    return rc;
+  GHIP(hipEventRecord(g->assembled, g->xfer[0]));
+  ++g->gathers_out;
+  return SRT_OK;
+}
+
+// The radiance rows to context 0 (only when the full accumulation image is asked for).
+int GatherAccum(srt_group* g) {
+  if (!g->accum_stale) return SRT_OK;
+  const int n = (int)g->ctx.size();
+  const size_t bytes = (size_t)g->rows_pad * g->W * 16;
+  if (!g->recv_acc) {
+    GHIP(hipSetDevice(g->dev[0]));
+    GHIP(hipMalloc(&g->recv_acc, (size_t)n * bytes));
+  }
+  if (int rc = Gather(g, g->band_accum, g->recv_acc, bytes, g->acc_sent)) return rc;
+  if (int rc = srt::AssembleBandsOn(g->ctx[0], g->xfer[0], g->recv_acc, n, g->rows_pad, g->band_rows, 1,
+                                    g->full_accum, nullptr))
+    return rc;
+  GHIP(hipEventRecord(g->assembled, g->xfer[0]));
+  ++g->gathers_acc;
+  g->accum_stale = false;
+  return SRT_OK;
 }
 
 }  // namespace
@@ -118,23 +283,24 @@ int srt_group_create(srt_context* const* ctxs, int n, int band_rows, srt_group**
   const char* tr = std::getenv("SRT_GROUP_TRANSPORT");
   const bool copy = repeated || (tr && std::string(tr) == "copy");
   if (!copy) {
-    g->comm.resize(n);
-    const ncclResult_t r = ncclCommInitAll(g->comm.data(), n, g->dev.data());
-    if (r != ncclSuccess) {
-      srt::SetError(std::string("group: ncclCommInitAll: ") + ncclGetErrorString(r));
+    const Rccl& R = rccl();
+    if (!R.ok) {
+      srt::SetError("group: " + R.err);
       delete g;
       return SRT_ERR_HIP;
     }
-  } else {
-    g->done.resize(n, nullptr);
-    for (int i = 0; i < n; ++i) {
-      if (hipSetDevice(g->dev[i]) != hipSuccess ||
-          hipEventCreateWithFlags(&g->done[i], hipEventDisableTiming) != hipSuccess) {
-        srt::SetError("group: hipEventCreate failed");
-        srt_group_destroy(g);
-        return SRT_ERR_HIP;
-      }
+    g->comm.resize(n);
+    const ncclResult_t r = R.CommInitAll(g->comm.data(), n, g->dev.data());
+    if (r != ncclSuccess) {
+      srt::SetError(std::string("group: ncclCommInitAll: ") + R.GetErrorString(r));
+      g->comm.clear();
+      delete g;
+      return SRT_ERR_HIP;
     }
+  }
+  if (int rc = CreateStreamsEvents(g)) {
+    srt_group_destroy(g);
+    return rc;
   }
   *out = g;
   return SRT_OK;
@@ -143,18 +309,56 @@ int srt_group_create(srt_context* const* ctxs, int n, int band_rows, srt_group**
 int srt_group_destroy(srt_group* g) {
   if (!g) return SRT_ERR_INVALID;
   (void)srt_group_finish(g);
+  // the contexts outlive the group: give each its own full-frame images back (and tiling 0 of 1), so
+  // that no context keeps a pointer to the band images freed below
+  if (!g->band_accum.empty())
+    for (srt_context* c : g->ctx) {
+      (void)srt_set_tiling(c, 0, 1, g->band_rows);
+      (void)srt_alloc_images(c);
+    }
   FreeImages(g);
-  for (ncclComm_t c : g->comm) (void)ncclCommDestroy(c);
-  for (size_t i = 0; i < g->done.size(); ++i) {
-    if (!g->done[i]) continue;
-    (void)hipSetDevice(g->dev[i]);
-    (void)hipEventDestroy(g->done[i]);
-  }
+  if (!g->comm.empty())
+    for (ncclComm_t c : g->comm) (void)rccl().CommDestroy(c);
+  DestroyStreamsEvents(g);
   delete g;
   return SRT_OK;
 }
 
 const char* srt_group_transport(srt_group* g) { return !g ? "" : g->comm.empty() ? "copy" : "rccl"; }
+
+int srt_group_get_int(srt_group* g, const char* name, int* v) {
+  if (!g || !name || !v) return SRT_ERR_INVALID;
+  const std::string k(name);
+  const int n = (int)g->ctx.size();
+  if (k == "contexts") {
+    *v = n;
+  } else if (k == "ranks") {
+    *v = n;
+    if (!g->comm.empty()) {
+      int count = 0;
+      GNCCL(rccl().CommCount(g->comm[0], &count));
+      *v = count;
+    }
+  } else if (k == "gathers.output") {
+    *v = (int)std::min<long long>(g->gathers_out, 0x7FFFFFFF);
+  } else if (k == "gathers.accum") {
+    *v = (int)std::min<long long>(g->gathers_acc, 0x7FFFFFFF);
+  } else if (k == "bytes.output") {
+    *v = (int)((size_t)n * g->rows_pad * g->W * 4 / 1024);
+  } else if (k == "bytes.accum") {
+    *v = (int)((size_t)n * g->rows_pad * g->W * 16 / 1024);
+  } else {
+    return SRT_ERR_NOT_FOUND;
+  }
+  return SRT_OK;
+}
+
+int srt_group_last_kernel_ms(srt_group* g, float* ms, int n) {
+  if (!g || !ms || n < 0) return SRT_ERR_INVALID;
+  for (int i = 0; i < n && i < (int)g->ctx.size(); ++i)
+    if (int rc = srt_last_kernel_ms(g->ctx[i], ms + i)) return rc;
+  return SRT_OK;
+}
 
 int srt_group_set_bool(srt_group* g, const char* name, int v) {
   if (!g) return SRT_ERR_INVALID;
@@ -196,25 +400,30 @@ int srt_group_alloc_images(srt_group* g) {
       return SRT_ERR_INVALID;
     }
   }
+  if (int rc = srt_group_finish(g)) return rc;
   FreeImages(g);
   g->W = W;
   g->H = H;
+  g->cur = 0;
+  g->accum_stale = false;
   const int bands = (H + g->band_rows - 1) / g->band_rows;
   g->rows_pad = ((bands + n - 1) / n) * g->band_rows;  // every context's local rows fit, padded equal
   const size_t band_px = (size_t)g->rows_pad * W, full_px = (size_t)W * H;
   g->band_accum.assign(n, nullptr);
-  g->band_out.assign(n, nullptr);
+  for (auto& bo : g->band_out) bo.assign(n, nullptr);
   for (int i = 0; i < n; ++i) {
     if (int rc = srt_set_tiling(g->ctx[i], i, n, g->band_rows)) return rc;
     GHIP(hipSetDevice(g->dev[i]));
     GHIP(hipMalloc(&g->band_accum[i], band_px * 16));
-    GHIP(hipMalloc(&g->band_out[i], band_px * 4));
     GHIP(hipMemset(g->band_accum[i], 0, band_px * 16));
-    GHIP(hipMemset(g->band_out[i], 0, band_px * 4));
-    if (int rc = srt_set_image_buffers(g->ctx[i], g->band_accum[i], g->band_out[i])) return rc;
+    for (auto& bo : g->band_out) {
+      GHIP(hipMalloc(&bo[i], band_px * 4));
+      GHIP(hipMemset(bo[i], 0, band_px * 4));
+    }
+    if (int rc = srt_set_image_buffers(g->ctx[i], g->band_accum[i], g->band_out[0][i])) return rc;
   }
   GHIP(hipSetDevice(g->dev[0]));
-  GHIP(hipMalloc(&g->recv, (size_t)n * band_px * 16));
+  GHIP(hipMalloc(&g->recv_out, (size_t)n * band_px * 4));
   GHIP(hipMalloc(&g->full_accum, full_px * 16));
   GHIP(hipMalloc(&g->full_out, full_px * 4));
   GHIP(hipMemset(g->full_accum, 0, full_px * 16));
@@ -223,25 +432,41 @@ int srt_group_alloc_images(srt_group* g) {
 }
 
 int srt_group_dispatch(srt_group* g, uint32_t gx, uint32_t gy) {
-  if (!g || !g->recv) return SRT_ERR_STATE;
+  if (!g || !g->recv_out) return SRT_ERR_STATE;
+  if (int rc = PrepareLaunch(g, g->cur)) return rc;
   for (srt_context* c : g->ctx)
     if (int rc = srt_dispatch(c, gx, gy)) return rc;
-  int frames = 0, reset = 0;
-  srt_get_int(g->ctx[0], "accumFrames", &frames);
+  g->accum_stale = true;
+  int reset = 0;
   srt_get_int(g->ctx[0], "resetAccumBuffer", &reset);
-  return GatherAssemble(g, frames, !reset);
+  if (reset) return SRT_OK;  // the reset dispatch stores no image0 pixel
+  const int ext_w = (int)std::min<uint64_t>((uint64_t)gx * 8, (uint64_t)g->W);
+  const int ext_h = (int)std::min<uint64_t>((uint64_t)gy * 8, (uint64_t)g->H);
+  const int rc = GatherOutput(g, g->cur, ext_w, ext_h);
+  g->cur ^= 1;
+  return rc;
 }
 
 int srt_group_render_frames(srt_group* g, int frame_first, int nframes) {
-  if (!g || !g->recv) return SRT_ERR_STATE;
-  for (srt_context* c : g->ctx)
-    if (int rc = srt_render_frames(c, frame_first, nframes, 0, 0)) return rc;
+  if (!g || !g->recv_out) return SRT_ERR_STATE;
+  if (nframes < 0 || frame_first < 1) return SRT_ERR_INVALID;
   if (nframes == 0) return SRT_OK;
-  return GatherAssemble(g, frame_first + nframes - 1, true);
+  if (int rc = PrepareLaunch(g, g->cur)) return rc;
+  for (srt_context* c : g->ctx)
+    if (int rc = srt_render_frames(c, frame_first, nframes, 1, 0)) return rc;
+  g->accum_stale = true;
+  const int rc = GatherOutput(g, g->cur, g->W, g->H);
+  g->cur ^= 1;
+  return rc;
 }
 
 int srt_group_finish(srt_group* g) {
   if (!g) return SRT_ERR_INVALID;
+  for (size_t i = 0; i < g->xfer.size(); ++i) {
+    if (!g->xfer[i]) continue;
+    GHIP(hipSetDevice(g->dev[i]));
+    GHIP(hipStreamSynchronize(g->xfer[i]));
+  }
   for (srt_context* c : g->ctx)
     if (int rc = srt_finish(c)) return rc;
   return SRT_OK;
@@ -251,6 +476,7 @@ int srt_group_read_accum(srt_group* g, float* host, size_t bytes) {
   if (!g || !host || !g->full_accum) return SRT_ERR_INVALID;
   const size_t need = (size_t)g->W * g->H * 16;
   if (bytes < need) return SRT_ERR_INVALID;
+  if (int rc = GatherAccum(g)) return rc;
   if (int rc = srt_group_finish(g)) return rc;
   GHIP(hipSetDevice(g->dev[0]));
   GHIP(hipMemcpy(host, g->full_accum, need, hipMemcpyDeviceToHost));
@@ -269,6 +495,8 @@ int srt_group_read_output(srt_group* g, uint8_t* host, size_t bytes) {
 
 int srt_group_image_pointers(srt_group* g, void** accum_dev, void** out_dev) {
   if (!g) return SRT_ERR_INVALID;
+  if (accum_dev && g->full_accum)
+    if (int rc = GatherAccum(g)) return rc;
   if (accum_dev) *accum_dev = g->full_accum;
   if (out_dev) *out_dev = g->full_out;
   return SRT_OK;

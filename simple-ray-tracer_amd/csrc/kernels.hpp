@@ -678,4 +678,19 @@ __global__ __launch_bounds__(256) void assemble_kernel(const float4* gathered, i
   }
 }
 
+// The multi-GPU root's per-frame step: every rank encoded its own rows' sRGB8 (accumFrames is one
+// uniform for all), so the gather moves 4 B/px and the root only de-interleaves them.  Pixels outside
+// the dispatch extent keep their old values, as a partial glDispatchCompute leaves them.
+__global__ __launch_bounds__(256) void assemble_out_kernel(const uint32_t* gathered, int nranks, int rows_pad, int W,
+                                                           int H, int band_rows, int ext_w, int ext_h, uint32_t* out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)W * (size_t)H) return;
+  const int y = (int)(i / (size_t)W), x = (int)(i - (size_t)y * W);
+  if (x >= ext_w || y >= ext_h) return;
+  const int band = y / band_rows;
+  const int r = band % nranks;
+  const int ly = (band / nranks) * band_rows + (y - band * band_rows);
+  out[i] = gathered[((size_t)r * rows_pad + ly) * W + x];
+}
+
 }  // namespace srt

@@ -811,7 +811,10 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   kp.lbuf = c->d_lbuf;
   kp.trav_frac16 = ldsm ? c->trav_frac16 : c->trav_frac16_global;
   kp.bounce_cap = c->bounce_cap;
-  HIP_OK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_TOTAL, c->stream));
+  // (ST_POOLERR, the last entry, is sticky: a watchdog that fired in an earlier launch of this
+  // render must still reach srt_finish, which reads and clears it)
+  static_assert(srt::ST_POOLERR + 1 == srt::ST_TOTAL, "ST_POOLERR must stay the last stats entry");
+  HIP_OK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_POOLERR, c->stream));
   const int out_frames = kp.frame_first + kp.nframes - 1;
   const int nchunks = (kp.nframes + chunk - 1) / chunk;
   if (nchunks > c->batch_ctr_cap) {
@@ -891,22 +894,29 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
 }
 
 // Depth of each BVH (root depth 0) and index validation.
+// Every node some traversal can reach is checked: the trees of the BVH records and node 0's (the
+// ghost records past n_bvhs traverse from node 0, raytrace_compute.glsl:144-147).  `reach` marks
+// them; the layouts and the upload touch no other node, so an unreachable record may hold anything.
 int ValidateNodes(const srt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_tris, const srt_bvh_record* bvhs,
-                  uint32_t n_bvhs, int* max_depth, std::vector<std::pair<uint32_t, uint32_t>>* tri_ranges) {
+                  uint32_t n_bvhs, int* max_depth, std::vector<std::pair<uint32_t, uint32_t>>* tri_ranges,
+                  std::vector<uint8_t>* reach) {
   *max_depth = 0;
   tri_ranges->assign(n_bvhs, {0u, 0u});
+  reach->assign(n_nodes, 0);
   std::vector<std::pair<uint32_t, int>> st;
   std::vector<uint8_t> seen(n_nodes, 0);
-  for (uint32_t b = 0; b < n_bvhs; ++b) {
+  for (uint32_t b = 0; b <= n_bvhs; ++b) {  // b == n_bvhs: node 0's tree
     uint32_t lo = 0xFFFFFFFFu, hi = 0;
-    if (bvhs[b].first_index >= n_nodes) {
+    const uint32_t root = b < n_bvhs ? bvhs[b].first_index : 0u;
+    if (root >= n_nodes) {
       srt::SetError("BVH first_index out of range");
       return SRT_ERR_INVALID;
     }
-    st.push_back({bvhs[b].first_index, 0});
+    st.push_back({root, 0});
     while (!st.empty()) {
       auto [i, d] = st.back();
       st.pop_back();
+      (*reach)[i] = 1;
       *max_depth = std::max(*max_depth, d);
       const srt_bvh_node& n = nodes[i];
       if (n.prim_count > 0) {
@@ -927,7 +937,7 @@ int ValidateNodes(const srt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_tris, 
       }
     }
     std::fill(seen.begin(), seen.end(), 0);
-    (*tri_ranges)[b] = lo < hi ? std::make_pair(lo, hi) : std::make_pair(0u, 0u);
+    if (b < n_bvhs) (*tri_ranges)[b] = lo < hi ? std::make_pair(lo, hi) : std::make_pair(0u, 0u);
   }
   return SRT_OK;
 }
@@ -1001,13 +1011,13 @@ bool LayoutNodes(const srt_bvh_node* nodes, uint32_t n_nodes, const srt_bvh_reco
 // for two), zero records filling the gaps; larger leaves are not padded.  The
 // map is monotone, so the order is kept and a BVH's triangle range stays one
 // slot range.  Returns false (identity) when two leaves' ranges partly overlap.
-bool LayoutTris(const srt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_tris, std::vector<uint32_t>* slot,
-                uint32_t* n_slots) {
+bool LayoutTris(const srt_bvh_node* nodes, uint32_t n_nodes, const std::vector<uint8_t>& reach, uint32_t n_tris,
+                std::vector<uint32_t>* slot, uint32_t* n_slots) {
   constexpr uint32_t kUnset = 0xFFFFFFFFu;
   std::vector<uint32_t> owner(n_tris, kUnset), lead(n_tris, 0);
   for (uint32_t i = 0; i < n_nodes; ++i) {
     const srt_bvh_node& n = nodes[i];
-    if (n.prim_count == 0) continue;
+    if (n.prim_count == 0 || !reach[i]) continue;  // (ValidateNodes range-checked the reachable leaves)
     const uint32_t f = n.first_child_or_prim_index;
     if (lead[f] != 0 && lead[f] != n.prim_count) return false;  // two leaves from one triangle, different sizes
     if (lead[f] == n.prim_count) continue;                      // the same leaf again (a shared subtree)
@@ -1032,6 +1042,39 @@ bool LayoutTris(const srt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_tris, st
 }
 
 }  // namespace
+
+namespace srt {
+
+// The multi-GPU root's assembly kernels on a given stream (srt_assemble_bands /
+// srt_assemble_output_bands use the context's own; the device group its gather stream).
+int AssembleBandsOn(srt_context* c, void* stream, const void* gathered, int nranks, int rows_pad, int band_rows,
+                    int frames, void* accum_full, void* out_full) {
+  if (!c || !gathered || nranks < 1 || rows_pad < 1 || band_rows < 1 || frames < 1 || c->W <= 0 || c->H <= 0)
+    return SRT_ERR_INVALID;
+  HIP_OK(hipSetDevice(c->device));
+  const size_t n = (size_t)c->W * (size_t)c->H;
+  hipLaunchKernelGGL(srt::assemble_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const float4*>(gathered), nranks, rows_pad, c->W,
+                     c->H, band_rows, frames, static_cast<float4*>(accum_full), static_cast<uint32_t*>(out_full));
+  HIP_OK(hipGetLastError());
+  return SRT_OK;
+}
+
+int AssembleOutputOn(srt_context* c, void* stream, const void* gathered_rgba8, int nranks, int rows_pad,
+                     int band_rows, int ext_w, int ext_h, void* out_full) {
+  if (!c || !gathered_rgba8 || !out_full || nranks < 1 || rows_pad < 1 || band_rows < 1 || c->W <= 0 || c->H <= 0)
+    return SRT_ERR_INVALID;
+  HIP_OK(hipSetDevice(c->device));
+  const size_t n = (size_t)c->W * (size_t)c->H;
+  hipLaunchKernelGGL(srt::assemble_out_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint32_t*>(gathered_rgba8), nranks, rows_pad,
+                     c->W, c->H, band_rows, std::min(ext_w, c->W), std::min(ext_h, c->H),
+                     static_cast<uint32_t*>(out_full));
+  HIP_OK(hipGetLastError());
+  return SRT_OK;
+}
+
+}  // namespace srt
 
 // ===========================================================================
 // C ABI (context part)
@@ -1087,6 +1130,7 @@ int srt_create(int device, void* stream, srt_context** out) {
     c->own_stream = true;
   }
   if (hipMalloc(&c->d_stats, sizeof(unsigned long long) * srt::ST_TOTAL) != hipSuccess ||
+      hipMemset(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_TOTAL) != hipSuccess ||
       hipMalloc(&c->d_nan, sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(c->d_nan, 0, sizeof(unsigned long long)) != hipSuccess) {
     FreeDev(c->d_stats);
@@ -1249,6 +1293,7 @@ int srt_finish(srt_context* c) {
   if (c->pool_launched) {  // pool_kernel's watchdog (pool.hpp): a launch that overran its deadline
     unsigned long long err = 0;
     HIP_OK(hipMemcpy(&err, c->d_stats + srt::ST_POOLERR, sizeof(err), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemset(c->d_stats + srt::ST_POOLERR, 0, sizeof(err)));
     c->pool_launched = false;
     if (err) {
       srt::SetError("pool_kernel: watchdog expired (the render is incomplete)");
@@ -1333,7 +1378,8 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   }
   int depth = 0;
   std::vector<std::pair<uint32_t, uint32_t>> tri_ranges;
-  int rc = ValidateNodes(nodes, n_nodes, n_tris, bvhs, n_bvhs, &depth, &tri_ranges);
+  std::vector<uint8_t> reach;
+  int rc = ValidateNodes(nodes, n_nodes, n_tris, bvhs, n_bvhs, &depth, &tri_ranges, &reach);
   if (rc) return rc;
   HIP_OK(hipSetDevice(c->device));
   // nodes: 32-B records behind a 32-B pad so sibling pairs are 64-B aligned,
@@ -1376,7 +1422,8 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   std::vector<uint32_t> tslot;
   uint32_t n_tslots = n_tris;
   // (the slots stay below 3 n_tris: a gap is at most two records per leaf)
-  const bool tris_laid = tri_align && n_tris < (1u << 30) && LayoutTris(nodes, n_nodes, n_tris, &tslot, &n_tslots);
+  const bool tris_laid =
+      tri_align && n_tris < (1u << 30) && LayoutTris(nodes, n_nodes, reach, n_tris, &tslot, &n_tslots);
   auto tsl = [&](uint32_t t) { return tris_laid ? tslot[t] : t; };
   for (auto& r : tri_ranges)
     if (r.first < r.second) r = {tsl(r.first), tsl(r.second - 1) + 1};
@@ -1388,7 +1435,8 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   std::vector<float4> hn(2 * ((size_t)n_slots + 1 + srt::kNodePad), make_float4(0, 0, 0, 0));
   bool pairs_aligned = true;
   for (uint32_t i = 0; i < n_nodes; ++i) {
-    if (remap[i] == 0xFFFFFFFFu) continue;
+    // (a node no traversal reaches keeps a zero record: its indices were never range-checked)
+    if (remap[i] == 0xFFFFFFFFu || !reach[i]) continue;
     const srt_bvh_node& n = nodes[i];
     uint32_t first = n.first_child_or_prim_index;
     if (n.prim_count == 0) {  // internal: c0's slot, less 1 when c1 is internal (its pair then follows)
@@ -1424,7 +1472,8 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   c->n_treelets = 0;
   {
     uint32_t max_leaf_in = 0;
-    for (uint32_t i = 0; i < n_nodes; ++i) max_leaf_in = std::max(max_leaf_in, nodes[i].prim_count);
+    for (uint32_t i = 0; i < n_nodes; ++i)
+      if (reach[i]) max_leaf_in = std::max(max_leaf_in, nodes[i].prim_count);
     int td = c->treelet_depth;
     if (td == 0) {  // ~1 MB of nodes + triangles per treelet
       td = 1;
@@ -1558,7 +1607,8 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   c->n_mats = n_mats;
   c->stack_entries = depth + 1;
   uint32_t max_leaf = 0;
-  for (uint32_t i = 0; i < n_nodes; ++i) max_leaf = std::max(max_leaf, nodes[i].prim_count);
+  for (uint32_t i = 0; i < n_nodes; ++i)
+    if (reach[i]) max_leaf = std::max(max_leaf, nodes[i].prim_count);
   c->lds_ok = n_tslots < (1u << 24) && n_slots + srt::kNodePad < (1u << 24) && max_leaf < 256;
   c->pairs_aligned = pairs_aligned;
   c->scene_ok = true;
@@ -1800,15 +1850,14 @@ int srt_set_image_buffers(srt_context* c, void* accum_dev, void* out_dev) {
 
 int srt_assemble_bands(srt_context* c, const void* gathered, int nranks, int rows_pad, int band_rows, int frames,
                        void* accum_full, void* out_full) {
-  if (!c || !gathered || nranks < 1 || rows_pad < 1 || band_rows < 1 || frames < 1 || c->W <= 0 || c->H <= 0)
-    return SRT_ERR_INVALID;
-  HIP_OK(hipSetDevice(c->device));
-  const size_t n = (size_t)c->W * (size_t)c->H;
-  hipLaunchKernelGGL(srt::assemble_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream,
-                     static_cast<const float4*>(gathered), nranks, rows_pad, c->W, c->H, band_rows, frames,
-                     static_cast<float4*>(accum_full), static_cast<uint32_t*>(out_full));
-  HIP_OK(hipGetLastError());
-  return SRT_OK;
+  return c ? srt::AssembleBandsOn(c, c->stream, gathered, nranks, rows_pad, band_rows, frames, accum_full, out_full)
+           : SRT_ERR_INVALID;
+}
+
+int srt_assemble_output_bands(srt_context* c, const void* gathered_rgba8, int nranks, int rows_pad, int band_rows,
+                              void* out_full) {
+  return c ? srt::AssembleOutputOn(c, c->stream, gathered_rgba8, nranks, rows_pad, band_rows, c->W, c->H, out_full)
+           : SRT_ERR_INVALID;
 }
 
 int srt_image_pointers(srt_context* c, void** accum_dev, void** out_dev) {

@@ -73,6 +73,25 @@ __device__ __forceinline__ int f2i(float x) {
 }
 __device__ __forceinline__ bool isinf_f(float x) { return __builtin_fabsf(x) == __builtin_inff(); }
 
+#ifndef SRT_CONTRACT_HW
+#define SRT_CONTRACT_HW 0
+#endif
+#if SRT_CONTRACT_HW
+// ---- contract F: GLSL transcendentals as AMD's GPU compilers lower them ------
+// A measurement build, never the default (make CONTRACT=F: libsrt_amd_F.so; DESIGN.md section 3,
+// "Tolerance").  A GL/Vulkan driver on gfx9+ lowers GLSL sin/cos to the hardware instructions on the
+// argument in revolutions -- v_mul_f32 by 1/(2 pi), then v_sin_f32 / v_cos_f32, with no further range
+// reduction (LLVM AMDGPU LowerTrig; only GFX8 inserts v_fract_f32) -- and pow(x, y) to
+// v_exp_f32(y * v_log_f32(x)).  The random numbers of raytrace_utils.glsl:28-54 go through that sin at
+// |x| ~ 1e3-1e4, so F moves every path; the oracle cannot restate these instructions, so F is
+// compared with contract A on the GPU (tools/contract_f.py).
+__device__ __forceinline__ float sin_f(float x) { return __builtin_amdgcn_sinf(x * 0x1.45f306p-3f); }
+__device__ __forceinline__ float cos_f(float x) { return __builtin_amdgcn_cosf(x * 0x1.45f306p-3f); }
+__device__ __forceinline__ float pow_f(float x, float y) {
+  return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+}
+__device__ __forceinline__ float pow5_f(float x) { return pow_f(x, 5.0f); }
+#else
 // ---- sin / cos ------------------------------------------------------------
 // The contract's sin/cos, in fp32 with fused multiply-adds:
 // k = rint(x * 2/pi); r = x - k * pi/2 with pi/2 = P1 + P2 + P3 (each product
@@ -169,6 +188,7 @@ __device__ __forceinline__ float pow5_f(float x) {
   const double d2 = d * d;
   return x == 0.0f ? 0.0f : (float)((d2 * d2) * d);
 }
+#endif  // SRT_CONTRACT_HW
 
 }  // namespace dev
 }  // namespace srt

@@ -127,4 +127,10 @@ bool ProgressiveFrame(CameraState* cam, const Vec3& move, float rot_x, float rot
 
 void SetError(const std::string& msg);
 
+// pathtrace.hip: the multi-GPU root's assembly on a given HIP stream (group.cpp's gather stream)
+int AssembleBandsOn(srt_context* c, void* stream, const void* gathered, int nranks, int rows_pad, int band_rows,
+                    int frames, void* accum_full, void* out_full);
+int AssembleOutputOn(srt_context* c, void* stream, const void* gathered_rgba8, int nranks, int rows_pad,
+                     int band_rows, int ext_w, int ext_h, void* out_full);
+
 }  // namespace srt

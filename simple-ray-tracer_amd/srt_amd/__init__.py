@@ -493,6 +493,12 @@ class Compute:
                                        C.c_void_p(accum_full_dev) if accum_full_dev else None,
                                        C.c_void_p(out_full_dev) if out_full_dev else None), "assemble_bands")
 
+    def assemble_output_bands(self, gathered_rgba8_dev: int, nranks: int, rows_pad: int, band_rows: int,
+                              out_full_dev: int):
+        """The per-frame root step: de-interleave the ranks' gathered sRGB8 rows into the full image0."""
+        check(lib().srt_assemble_output_bands(self.ctx, C.c_void_p(gathered_rgba8_dev), nranks, rows_pad, band_rows,
+                                              C.c_void_p(out_full_dev)), "assemble_output_bands")
+
     # -- dispatch -------------------------------------------------------------
     def Dispatch(self, groups_x: int, groups_y: int, groups_z: int = 1):
         """glDispatchCompute(groups_x, groups_y, 1) (src/main.cpp:706)."""

@@ -124,6 +124,8 @@ _SIGS = {
     "srt_group_read_output": (C.c_int, [P, P, C.c_size_t]),
     "srt_group_image_pointers": (C.c_int, [P, C.POINTER(P), C.POINTER(P)]),
     "srt_group_transport": (C.c_char_p, [P]),
+    "srt_group_get_int": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_int)]),
+    "srt_group_last_kernel_ms": (C.c_int, [P, C.POINTER(C.c_float), C.c_int]),
     "srt_upload_scene": (C.c_int, [P, P, C.c_uint32, P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P,
                                    C.c_uint32]),
     "srt_upload_textures": (C.c_int, [P, C.POINTER(Texture), C.c_uint32]),
@@ -140,6 +142,7 @@ _SIGS = {
     "srt_image_pointers": (C.c_int, [P, C.POINTER(P), C.POINTER(P)]),
     "srt_set_image_buffers": (C.c_int, [P, P, P]),
     "srt_assemble_bands": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
+    "srt_assemble_output_bands": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P]),
     "srt_trace_closest": (C.c_int, [P, P, C.c_uint32, P, P]),
     "srt_model_load": (C.c_int, [C.c_char_p, C.POINTER(P)]),
     "srt_model_load_ex": (C.c_int, [C.c_char_p, C.c_uint32, C.POINTER(P)]),
@@ -190,10 +193,12 @@ def lib() -> C.CDLL:
         # first and torch's CUDA later left torch on a runtime it was not built against, and the
         # process aborted at exit ("free(): invalid pointer") after a test had used torch.cuda
         # buffers; with torch loaded first, as bench.py does, both run on torch's runtime.
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
+        # A pure C-ABI user that never touches torch may skip it: SRT_PRELOAD_TORCH=0.
+        if os.environ.get("SRT_PRELOAD_TORCH", "1") != "0":
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
         handle = C.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | C.RTLD_GLOBAL)
         for name, (res, args) in _SIGS.items():
             fn = getattr(handle, name)

@@ -142,6 +142,43 @@ class GroupRenderer:
 
         return lib().srt_group_transport(self.g).decode()
 
+    def get_int(self, name: str) -> int:
+        """srt_group_get_int: "contexts", "ranks" (RCCL's communicator count), "gathers.output",
+        "gathers.accum", "bytes.output" / "bytes.accum" (KiB one such gather moves)."""
+        import ctypes as C
+
+        from ._lib import check, lib
+
+        v = C.c_int()
+        check(lib().srt_group_get_int(self.g, name.encode(), C.byref(v)), "group_get_int")
+        return int(v.value)
+
+    def kernel_ms(self) -> list[float]:
+        """Each context's sample-kernel device time in the last render (HIP events on its stream)."""
+        import ctypes as C
+
+        from ._lib import check, lib
+
+        ms = (C.c_float * len(self.parts))()
+        check(lib().srt_group_last_kernel_ms(self.g, ms, len(self.parts)), "group_last_kernel_ms")
+        return [float(x) for x in ms]
+
+    def count(self, spp: int) -> dict:
+        """Untimed counting render (the counting instance on every context, CheckHit counts summed) of
+        the reset frame + `spp` frames.  The contexts' radiance is left at the rendered frame; the group's
+        image0 is not assembled (the timed renders that follow do that)."""
+        self.finish()
+        self.clear()
+        for p in self.parts:
+            p.compute.render_frames(2, spp, write_output=True, count=True)
+        self.accum_frames = spp + 1
+        self.finish()
+        tot: dict = {}
+        for p in self.parts:
+            for k, v in p.compute.stats().items():
+                tot[k] = max(tot.get(k, 0), v) if k == "max_stack" else tot.get(k, 0) + v
+        return tot
+
     @property
     def groups(self):
         s = self.setup

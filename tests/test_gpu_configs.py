@@ -15,8 +15,12 @@ Configs (BASELINE.json "configs"):
                                                                its materials are pinned by test_airplane_*
   C4 Rubik 4096x4096 @ 1024 spp, maxDepth 8, 8 ranks        -- full render, oracle rows at 1024 spp,
                                                                8-way band split reassembled
-  C5 synthetic 10 M triangles 4096x4096 (512 spp in the config) -- full frame at 2 spp, oracle rows,
-                                                               determinism
+  C5 synthetic 10 M triangles 4096x4096 (512 spp in the config) -- full frame at the bench's 16 spp,
+                                                               oracle rows, determinism
+  C3 stand-in: torus-knot surface mesh 1920x1080 @ 256 spp      -- C3's regime (global-scene mode, real
+                                                               surface mesh) at C3's size, oracle rows
+Every render goes through the counting instance and then the timed instance the benchmark measures at
+that size, which must agree bit for bit.
 """
 import numpy as np
 import pytest
@@ -29,12 +33,41 @@ from conftest import OBJECTS, bits_equal, oracle_render
 pytestmark = pytest.mark.gpu
 
 
-def gpu_render(setup, spp, **kw):
+def gpu_render(setup, spp, *, timed=True, count=True, **kw):
+    """The frame through the counting instance (with its CheckHit counts), then again through the timed
+    instance bench.py measures at this size (sphere_kernel, the LDS kernel, global-scene mode's fused or IL
+    instance at the scene's wave count), which must give the same frame bit for bit.  count=False renders
+    the timed instance alone (stats empty)."""
     r = R.Renderer(setup, **kw)
     try:
-        r.render(spp, count=True)
-        r.finish()
-        return r.accum(), r.output(), r.compute.stats()
+        acc = out = None
+        st = {}
+        if count:
+            r.render(spp, count=True)
+            r.finish()
+            acc, out, st = r.accum(), r.output(), r.compute.stats()
+        if timed or not count:
+            r.render(spp)
+            r.finish()
+            tacc, tout = r.accum(), r.output()
+            if acc is not None:
+                eq = bits_equal(tacc, acc)
+                assert eq.all(), f"timed instance: {(~eq).sum()} accumulation values differ from the counting one"
+                assert (tout == out).all()
+            acc, out = tacc, tout
+        return acc, out, st
+    finally:
+        r.close()
+
+
+def timed_instance(setup) -> str:
+    """The instance bench.py's timed launches take for this setup (srt_get_int's scene.* names)."""
+    r = R.Renderer(setup)
+    try:
+        c = r.compute
+        if not setup.show_model:
+            return "sphere"
+        return f"fused{c.GetInt('scene.global_waves')}" if c.GetInt("scene.fused") == 1 else "IL"
     finally:
         r.close()
 
@@ -61,6 +94,7 @@ def test_c1_spheres_256_1spp_full_frame():
 
 def test_c2_spheres_1024_64spp_depth4():
     setup = R.make_setup(1024, 1024, show_model=False, max_depth=4)
+    assert timed_instance(setup) == "sphere"
     gacc, gout, gst = gpu_render(setup, 64)
     rows = spread_rows(1024, 24)
     acc, out, st = oracle_render(setup, 64, rows=rows)
@@ -104,7 +138,7 @@ def test_c4_rubik_4096_1024spp_depth8_rows_and_8_rank_split():
     assert_rows(gacc, gout, acc, out, rows)
     # the 8-GPU split of the config, rank by rank on one GPU (bench.py's 2-row bands)
     band, nranks = 2, 8
-    parts = [gpu_render(setup, spp, rank=r, nranks=nranks, band_rows=band)[0] for r in range(nranks)]
+    parts = [gpu_render(setup, spp, count=False, rank=r, nranks=nranks, band_rows=band)[0] for r in range(nranks)]
     facc, fout = _assemble(setup, parts, band, spp)
     assert bits_equal(facc, gacc).all()
     assert (fout == gout).all()
@@ -119,18 +153,36 @@ def c5_setup():
 
 
 def test_c5_synthetic_10M_rows_and_determinism(c5_setup):
-    """C5 at its full frame size and scene; 2 spp of its 512 (the rate, not the image, is the config's point)."""
+    """C5 at its full frame size and scene, at the bench's 16 spp of its 512 (the rate, not the image, is the
+    config's point): the counting and the timed IL instance (tile-major order, compiled in only for trees
+    past 600 MB) bit-equal, oracle rows across the frame, and two full renders identical."""
     setup = c5_setup
-    spp = 2
+    assert timed_instance(setup) == "IL"
+    spp = 16
     a, o, st = gpu_render(setup, spp)
     assert st["samples"] == 4096 * 4096 * spp and st["stack_overflow"] == 0
     assert st["max_stack"] > 0
     rows = spread_rows(4096, 6)
     acc, out, _ = oracle_render(setup, spp, rows=rows)
     assert_rows(a, o, acc, out, rows)
-    b, p, st2 = gpu_render(setup, spp)
+    b, p, _ = gpu_render(setup, spp, count=False)
     assert bits_equal(a, b).all() and (o == p).all()
-    assert st2["rays"] == st["rays"] and st2["nodes"] == st["nodes"] and st2["tris"] == st["tris"]
+
+
+def test_c3_standin_surface_mesh_1080p_256spp():
+    """C3's regime (the Airplane OBJ is absent: .MISSING_LARGE_BLOBS): a real surface mesh in global-scene
+    mode at C3's frame and spp, 1920x1080 @ 256 spp -- the bench's surface-mesh scene (torus-knot tube,
+    262,144 triangles, model camera and lights) through the timed fused instance at 5 waves per SIMD, bit-equal
+    to the counting instance over the whole frame and to the oracle on rows spread across it."""
+    setup = R.make_setup(1920, 1080, show_model=True, models=[R.torus_knot_model()])
+    assert timed_instance(setup) == "fused5"
+    spp = 256
+    a, o, st = gpu_render(setup, spp)
+    assert st["samples"] == 1920 * 1080 * spp and st["stack_overflow"] == 0
+    rows = spread_rows(1080, 12)
+    acc, out, _ = oracle_render(setup, spp, rows=rows)
+    assert_rows(a, o, acc, out, rows)
+    assert st["tris"] > st["samples"]  # (the mesh covers much of the frame: more triangle tests than samples)
 
 
 def _coincident_star(n=300, seed=5):

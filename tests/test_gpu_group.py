@@ -92,3 +92,125 @@ def test_cpp_compute_group_main_loop(setup, want, tmp_path, devices):
     acc = np.fromfile(tmp_path / "g.accum", np.float32).reshape(48, 64, 4)
     out = np.fromfile(tmp_path / "g.rgba8", np.uint8).reshape(48, 64, 4)
     assert bits_equal(acc, want[0]).all() and (out == want[1]).all()
+
+
+def _oracle_frames(setup, n):
+    """The oracle's frame (accum, out) after each of n progressive dispatches (reset frame first)."""
+    from oracle import pyoracle as O
+
+    s = setup
+    orc = O.Oracle(s.scene, s.lights, s.noise, s.noise_u)
+    cam = s.camera
+    f = O.Oracle.frame(s.width, s.height, show_model=s.show_model, bvh_count=s.bvh_count, light_count=len(s.lights),
+                       max_depth=s.max_depth, origin=cam.position, direction=cam.front, up=cam.up, right=cam.right)
+    import numpy as np
+
+    acc = np.zeros((s.height, s.width, 4), np.float32)
+    out = np.zeros((s.height, s.width, 4), np.uint8)
+    f.reset, f.accum_frames = 1, 1
+    orc.dispatch(f, acc, out)
+    f.reset = 0
+    frames = []
+    for k in range(2, n + 2):
+        orc.render(f, k, 1, acc, out)
+        frames.append((acc.copy(), out.copy()))
+    return frames
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+def test_group_every_intermediate_frame(setup, devices):
+    """srt_group_dispatch frame by frame, image0 read after every frame (the copy transport's
+    write-after-read race could mix bands of frames N and N+1; the sRGB8 band images are now double-buffered
+    with each render waiting for the gather that last read its buffer).  Every frame is the oracle's; only
+    image0 crosses per frame, the radiance once, when it is read."""
+    want = _oracle_frames(setup, 5)
+    g = R.GroupRenderer(setup, devices, band_rows=8)
+    try:
+        g.clear()
+        outs = []
+        for _ in range(5):
+            g.frame()
+            outs.append(g.output())  # (finishes the group, then copies image0)
+        assert g.get_int("gathers.output") == 5 and g.get_int("gathers.accum") == 0
+        assert g.get_int("bytes.accum") == 4 * g.get_int("bytes.output")
+        acc = g.accum()
+        assert g.get_int("gathers.accum") == 1
+        assert g.get_int("ranks") == len(devices)
+    finally:
+        g.close()
+    for k, (wa, wo) in enumerate(want):
+        assert (outs[k] == wo).all(), f"frame {k + 1}: image0 differs from the oracle's"
+    assert bits_equal(acc, want[-1][0]).all()
+
+
+def test_group_frames_back_to_back_without_reads(setup):
+    """Five dispatches enqueued with no host sync between them (frame k's gather runs beside frame k+1's
+    render on three contexts of one device), then one read: the oracle's frame."""
+    want = _oracle_frames(setup, 5)[-1]
+    g = R.GroupRenderer(setup, [0, 0, 0], band_rows=2)
+    try:
+        g.clear()
+        for _ in range(5):
+            g.frame()
+        acc, out = g.accum(), g.output()
+    finally:
+        g.close()
+    assert bits_equal(acc, want[0]).all() and (out == want[1]).all()
+
+
+def test_group_destroy_gives_contexts_their_images_back(setup, want):
+    """After srt_group_destroy the caller's contexts own full-frame images again (rank 0 of 1) and render
+    the whole frame (they kept pointers to the freed band images)."""
+    import ctypes as C
+
+    from srt_amd._lib import check, lib
+
+    parts = [R.Renderer(setup) for _ in range(2)]
+    try:
+        ctxs = (C.c_void_p * 2)(*[p.compute.ctx for p in parts])
+        g = C.c_void_p()
+        check(lib().srt_group_create(ctxs, 2, 8, C.byref(g)), "group_create")
+        check(lib().srt_group_alloc_images(g), "group_alloc_images")
+        check(lib().srt_group_destroy(g), "group_destroy")
+        for p in parts:
+            assert p.compute.local_rows() == setup.height
+            p.render(3)
+            p.finish()
+            assert bits_equal(p.accum(), want[0]).all() and (p.output() == want[1]).all()
+    finally:
+        for p in parts:
+            p.close()
+
+
+def test_bench_in_process_group_same_device(tmp_path):
+    """`python bench.py --gpus 4 --same-device` without torch.distributed: the in-process device group
+    (four contexts on GPU 0, device-copy transport) renders the one-GPU frame bit for bit, and the line
+    names the transport, the ranks and every rank's kernel time."""
+    import json
+    import subprocess
+    import sys
+
+    import numpy as np
+
+    from conftest import ROOT
+
+    W, H, SPP = 96, 61, 3
+    frames = {}
+    lines = {}
+    for n in (1, 4):
+        dump = tmp_path / f"f{n}.npz"
+        cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--steps", "2", "--warmup", "1",
+               "--width", str(W), "--height", str(H), "--spp", str(SPP), "--band-rows", "2", "--no-cpu-baseline",
+               "--no-global-leg", "--no-surface-leg", "--same-device", "--dump", str(dump)]
+        env = {k: v for k, v in __import__("os").environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+        res = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=env)
+        assert res.returncode == 0, res.stderr[-3000:]
+        lines[n] = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
+        with np.load(dump) as z:
+            frames[n] = (z["accum"], z["out"])
+    assert bits_equal(frames[4][0], frames[1][0]).all() and (frames[4][1] == frames[1][1]).all()
+    j = lines[4]
+    assert j["n_gpus"] == 4 and j["value"] > 0
+    assert j["group"]["transport"] == "copy" and j["group"]["rccl_ranks"] == 4 and j["group"]["contexts"] == 4
+    assert len(j["kernel_ms_per_rank"]) == 4 and all(v > 0 for v in j["kernel_ms_per_rank"])
+    assert j["group"]["radiance_gathers_in_timed_steps"] == 0

@@ -305,6 +305,31 @@ def test_triangle_slots_unusual_leaves(case):
     assert_parity(mod, 2)
 
 
+@pytest.mark.parametrize("layout", ["1", "0"])
+def test_unreachable_garbage_nodes(monkeypatch, layout):
+    """Records no traversal reaches may hold anything: a leaf whose triangle range lies far past
+    the array and an internal node whose children do, appended to a soup's node array.  The upload checks
+    and lays out (triangle slots forced on; node layout laid out or kept) only the nodes reachable from
+    the BVH roots and node 0, and the frame is the oracle's."""
+    import dataclasses
+
+    monkeypatch.setenv("SRT_TRI_ALIGN", "1")
+    monkeypatch.setenv("SRT_NODE_LAYOUT", layout)
+    setup = R.make_setup(48, 40, show_model=True, models=[R.synthetic_model(30000, seed=3)])
+    n = setup.scene.nodes
+    m = np.zeros(len(n) + 2, dtype=n.dtype)
+    m[:len(n)] = n
+    m["first"][-2], m["count"][-2] = 0xFFFFFF00, 5     # a leaf past the triangles
+    m["first"][-1], m["count"][-1] = 0xFFFFFFF0, 0     # an internal node past the nodes
+    mod = dataclasses.replace(setup, scene=dataclasses.replace(setup.scene, nodes=m))
+    r = R.Renderer(mod)
+    try:
+        assert r.compute.GetInt("scene.tri_slots") > 30000
+    finally:
+        r.close()
+    assert_parity(mod, 2)
+
+
 def test_global_schedule_chosen_by_scene_size():
     """srt_upload_scene's choices for the timed global-scene instance, as bench.py reports them: the torus
     knot (20 MB of nodes + triangles) takes fused sub-steps at 5 waves per SIMD, a 1 M soup (101 MB)

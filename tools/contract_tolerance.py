@@ -17,7 +17,14 @@ on the metric frame (Rubik 1920x1080, model camera, 6 lights, maxDepth 5), every
 and reports per-pixel L2 of the mean radiance accum/N between A and each other render (mean, p50, p99,
 max), the image-mean difference per channel with its standard error, at several sample counts.
 
-TEST INFRASTRUCTURE: it runs the oracle only (no GPU).  Output: JSON (default profiles/r03_contract_tolerance.json).
+Two comparisons per variant X:
+  X           X on A's own frames (2..): the primary rays' jitter and, until the paths part, every random
+              number are shared with A, so X sits closer to A than a resampling does by construction;
+  X_disjoint  X on the next frames (2 + N..), A' 's frames: like for like with A', so any excess of
+              X_disjoint over A' (L2) or any image-mean offset beyond its standard error is the
+              contract's own effect (--no-disjoint skips these).
+
+TEST INFRASTRUCTURE: it runs the oracle only (no GPU).  Output: JSON (default profiles/r04_contract_tolerance.json).
 """
 from __future__ import annotations
 
@@ -77,7 +84,8 @@ def main(argv=None):
     ap.add_argument("--spp", default="16,64,256")
     ap.add_argument("--contracts", default="B,C,D,E")
     ap.add_argument("--threads", type=int, default=0)
-    ap.add_argument("--out", default=str(ROOT / "profiles" / "r03_contract_tolerance.json"))
+    ap.add_argument("--no-disjoint", action="store_true")
+    ap.add_argument("--out", default=str(ROOT / "profiles" / "r04_contract_tolerance.json"))
     args = ap.parse_args(argv)
     from srt_amd import render as R
 
@@ -91,6 +99,8 @@ def main(argv=None):
     renders = {}
     for c in args.contracts.split(","):
         renders[c], _ = render_rows(setup, c, rows, 2, marks, threads)
+        if not args.no_disjoint:
+            renders[c + "_disjoint"], _ = render_rows(setup, c, rows, 2 + marks[-1], marks, threads)
         print(f"contract {c} done ({time.time() - t0:.0f} s)", file=sys.stderr, flush=True)
     # A': the same contract on the next frames (an independent resampling of every pixel)
     renders["A_resampled"], _ = render_rows(setup, "A", rows, 2 + marks[-1], marks, threads)
@@ -100,7 +110,8 @@ def main(argv=None):
            "contracts": {"A": "kernel contract (dot/cross fused, fp32 FMA sin/cos)",
                          "B": "no FMA in any expression", "C": "every a*b+c fused (gcc -ffp-contract=fast -mfma)",
                          "D": "sin/cos in double rounded to float", "E": "B + D (the round-1 contract)",
-                         "A_resampled": "contract A, next frames: Monte-Carlo resampling floor"},
+                         "A_resampled": "contract A, next frames: Monte-Carlo resampling floor",
+                         "X_disjoint": "contract X on A_resampled's frames: like-for-like with A_resampled"},
            "rays_A": int(rays_a), "seconds": round(time.time() - t0, 1),
            "mean_radiance_A": {str(n): float(np.mean(np.sqrt(np.sum(base[n] ** 2, axis=-1)))) for n in marks},
            "by_spp": {}}
