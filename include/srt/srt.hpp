@@ -174,7 +174,8 @@ class Compute {
 
 // The frame of main.cpp's loop tiled over several GPUs of this process (srt_group_*): one
 // Compute per device; uniforms and bindings go to every device; Dispatch / RenderFrames render each
-// device's row bands, gather them to the first device over RCCL and assemble the full frame there.
+// device's row bands and their sRGB8, gather those (4 B/px) to the first device over RCCL and assemble
+// the full image0 there; the radiance is gathered only by ReadAccum.
 //   Graphics::ComputeGroup rt("./shaders/raytrace_compute.glsl", {0, 1, 2, 3, 4, 5, 6, 7});
 //   rt.ForEach([&](Graphics::Compute& c) { c.Use(); AssetUtils::UploadModelDataToGPU({model.get()}, 5); });
 //   ... rt.SetInt("accumFrames", accumFrames); rt.Dispatch(W / 8, H / 8); rt.Finish(); ...
@@ -205,6 +206,17 @@ class ComputeGroup {
     return g_;
   }
   const char* Transport() { return srt_group_transport(group()); }
+  // ranks RCCL sees (or the contexts, under the copy transport), and each device's kernel time
+  int Ranks() {
+    int v = 0;
+    check(srt_group_get_int(group(), "ranks", &v), "ComputeGroup::Ranks");
+    return v;
+  }
+  std::vector<float> KernelMs() {
+    std::vector<float> v(parts_.size());
+    check(srt_group_last_kernel_ms(group(), v.data(), (int)v.size()), "ComputeGroup::KernelMs");
+    return v;
+  }
 
   void SetBool(const std::string& n, bool v) { ForEach([&](Compute& c) { c.SetBool(n, v); }); }
   void SetInt(const std::string& n, int v) {

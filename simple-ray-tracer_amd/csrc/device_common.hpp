@@ -44,10 +44,6 @@ struct KParams {
   // pair's start - 1) flags a right child whose own pair follows (pathtrace.hip
   // LayoutNodes); ref_or = 1 decodes it, 0 for the identity layout (no flags)
   uint32_t ref_or;
-  // global-scene mode, laid-out node arrays: every sibling pair whose right child is a leaf of one or
-  // two triangles is followed by copies of those triangle records (pathtrace.hip LayoutNodes), so the
-  // fused step that expands the parent tests that leaf from the same memory round trip (trav_fused)
-  int inline_leaves;
   float4* lbuf;            // sample buffer: nframes x local_pixels radiance samples
   int local_pixels;        // W * local_rows
   int trav_frac16;         // resume shading when fewer than trav_frac16/16 of working lanes traverse

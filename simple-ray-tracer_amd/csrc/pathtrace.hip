@@ -88,7 +88,6 @@ struct srt_context {
   std::vector<std::pair<uint32_t, uint32_t>> bvh_tris;  // triangle range [lo, hi) of each record's tree
   uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
   uint32_t ref_or = 0;  // KParams::ref_or of the uploaded node layout
-  bool inline_leaves = false;  // KParams::inline_leaves of the uploaded node layout
   // textures (srt_upload_textures) and, when materials sample them, the
   // per-triangle vertex uvs (2 float4: uv0 uv1 | uv2 0 0)
   float4* d_tex = nullptr;
@@ -137,7 +136,7 @@ struct srt_context {
   int trav_frac16 = 9;                 // SRT_TRAV_FRAC16 (measured best on Rubik 1080p with the 16-sub-step pattern)
   int bounce_cap = 1 << 20;            // SRT_BOUNCE_CAP: bounces after which a path is cut (counted)
   int trav_frac16_global = 9;          // SRT_TRAV_FRAC16_GLOBAL: the same threshold for global-scene mode
-  bool trav_frac16_global_env = false; // (set: every global instance uses it; else the fused 4-wave one takes 7)
+  bool trav_frac16_global_env = false; // (set: every global instance uses it; else the fused 4-wave one takes 7, the timed IL one 8)
   bool pool_launched = false;          // the last render ran pool_kernel (srt_finish checks its watchdog)
   int pool = 0;                        // SRT_POOL=1: LDS mode runs pool_kernel (workgroup ray pools)
   int pool_batch = 64;                 // SRT_POOL_BATCH: queued hits a shading wave waits for
@@ -367,7 +366,6 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
   kp->nodes_f4 = (int)(2 * ((size_t)c->n_nodes + 1));
   kp->nodes_lds_f4 = (int)((((size_t)kp->nodes_f4 + 3) >> 2) * srt::kNodeBlkF4);  // padded pair blocks
   kp->ref_or = c->ref_or;
-  kp->inline_leaves = c->inline_leaves ? 1 : 0;
   kp->tris_f4 = (int)(3 * ((size_t)c->n_tris + srt::kTriPad));  // with the padding records
   CameraParams(c, kp);
   return SRT_OK;
@@ -427,6 +425,10 @@ int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
   // (torus knot) and IL (C5) instances lose
   if constexpr (!LDSM && FUSE && GW == 4)
     if (!c->trav_frac16_global_env) kp.trav_frac16 = 7;
+  // ... and of the timed IL instance (trees past 600 MB): 8 (C5, kernel ms on one box: 9 771-773,
+  // 8 762-767, 10 793; profiles/r03_experiments/c5_pattern_threshold.txt)
+  if constexpr (!LDSM && !FUSE && !COUNT)
+    if (!c->trav_frac16_global_env) kp.trav_frac16 = 8;
   HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
   hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX, FUSE, GW>), dim3(blocks), dim3(BLOCK), lds, c->stream,
                      kp);
@@ -959,13 +961,8 @@ int ValidateNodes(const srt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_tris, 
 // reference-built tree has.  A child pair reached from two BVH records' trees
 // keeps its first placement; srt_upload_scene sets a node's "right child's
 // pair follows" flag only where the remapped slots confirm it.
-// `inl` (global-scene mode, trav_fused): a pair whose right child is a leaf of one or two
-// triangles is followed by 4 slots (128 B) that will hold copies of those triangle records (96 B,
-// then a zero slot keeping the next pair 64-B aligned); `inl_pairs` lists those pairs' c0.
 bool LayoutNodes(const srt_bvh_node* nodes, uint32_t n_nodes, const srt_bvh_record* bvhs, uint32_t n_bvhs,
-                 bool align, std::vector<uint32_t>* remap, uint32_t* n_slots, bool inl = false,
-                 std::vector<uint32_t>* inl_pairs = nullptr) {
-  if (inl_pairs) inl_pairs->clear();
+                 bool align, std::vector<uint32_t>* remap, uint32_t* n_slots) {
   constexpr uint32_t kUnset = 0xFFFFFFFFu;
   remap->assign(n_nodes, kUnset);
   auto& m = *remap;
@@ -998,10 +995,6 @@ bool LayoutNodes(const srt_bvh_node* nodes, uint32_t n_nodes, const srt_bvh_reco
         m[c0] = next;
         m[c1] = next + 1;
         next += 2;
-        if (inl && nodes[c1].prim_count - 1u < 2u) {  // c1: a leaf of 1 or 2 triangles
-          inl_pairs->push_back(c0);
-          next += 4;
-        }
         chain_next = nodes[c1].prim_count == 0 ? c1 : kUnset;
         st.push_back(c0);  // popped after c1's subtree: c1 is visited first
         st.push_back(c1);
@@ -1259,7 +1252,6 @@ int srt_get_int(srt_context* c, const char* name, int* v) {
   else if (n == "scene.wf_waves") *v = c->wf_waves;
   else if (n == "scene.treelets") *v = (int)c->n_treelets;
   else if (n == "scene.tri_slots") *v = (int)c->n_tris;  // device triangle records (LayoutTris gaps included)
-  else if (n == "scene.inline_leaves") *v = c->inline_leaves ? 1 : 0;
   else return SRT_ERR_NOT_FOUND;
   return SRT_OK;
 }
@@ -1423,17 +1415,7 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   // Crossover taken at 48 MB; SRT_GLOBAL_WAVES_MODE=4/5 forces either.
   const char* gw_env = std::getenv("SRT_GLOBAL_WAVES_MODE");
   c->global_waves = gw_env ? (gw_env[0] == '5' ? 5 : 4) : (scene_mb < 48.0 ? 5 : 4);
-  // Inline leaves (traversal.hpp trav_fused): the timed fused instance tests a right child that is
-  // a leaf of <= 2 triangles from the round trip that expands its parent.  For scenes read through
-  // L2 (never the LDS copy) whose schedule is fused, and not with treelets (their node copy walks
-  // every slot); SRT_INLINE_LEAVES=1/0 forces either.
-  const char* il_env = std::getenv("SRT_INLINE_LEAVES");
-  const bool inl = (il_env ? il_env[0] == '1' : (c->fused && scene_mb >= 1.0)) && c->treelets != 1 &&
-                   c->wavefront != 1;
-  std::vector<uint32_t> inl_pairs;
-  bool laid = !(lay_env && lay_env[0] == '0') &&
-              LayoutNodes(nodes, n_nodes, bvhs, n_bvhs, align, &remap, &n_slots, inl, &inl_pairs);
-  if (!laid) inl_pairs.clear();
+  bool laid = !(lay_env && lay_env[0] == '0') && LayoutNodes(nodes, n_nodes, bvhs, n_bvhs, align, &remap, &n_slots);
   // Triangle slots (LayoutTris) for every scene read through L2 (none of 1 MB fits the LDS copy):
   // fewer lines per leaf step (A/B on one box, kernel ms: C5 10 M 4096² 820 -> 773 with the IL leaf
   // step's own-record reads, 3 M 58.4 -> 56.5, 1 M 34.1 -> 32.6, torus knot 27.4 -> 27.4, Rubik
@@ -1454,8 +1436,7 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
     for (uint32_t i = 0; i < n_nodes; ++i) remap[i] = i;
     n_slots = n_nodes;
   }
-  // (+8 float4: a fused step reads up to 6 float4 past a pair, the inline records' place)
-  std::vector<float4> hn(2 * ((size_t)n_slots + 1 + srt::kNodePad) + 8, make_float4(0, 0, 0, 0));
+  std::vector<float4> hn(2 * ((size_t)n_slots + 1 + srt::kNodePad), make_float4(0, 0, 0, 0));
   bool pairs_aligned = true;
   for (uint32_t i = 0; i < n_nodes; ++i) {
     // (a node no traversal reaches keeps a zero record: its indices were never range-checked)
@@ -1593,12 +1574,6 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
     ht[3 * st + 1] = make_float4(e1[1], e1[2], e2[0], e2[1]);
     ht[3 * st + 2] = make_float4(e2[2], mf, tf, 0.0f);
   }
-  // inline leaves: copies of a right-child leaf's (<= 2) triangle records after its pair
-  for (uint32_t c0 : inl_pairs) {
-    const srt_bvh_node& leaf = nodes[c0 + 1];
-    const size_t dst = 2 * (size_t)remap[c0] + 6, src = 3 * (size_t)tsl(leaf.first_child_or_prim_index);
-    for (uint32_t k = 0; k < 3 * leaf.prim_count; ++k) hn[dst + k] = ht[src + k];
-  }
   // vertex uvs per triangle, for the materials that sample a texture
   std::vector<float4> huv;
   if (sampled) {
@@ -1632,7 +1607,6 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   c->bvhs_dirty = true;
   c->n_nodes = n_slots + srt::kNodePad;
   c->ref_or = laid ? 1u : 0u;
-  c->inline_leaves = !inl_pairs.empty();
   c->n_tris = n_tslots;  // device records (slots)
   c->n_mats = n_mats;
   c->stack_entries = depth + 1;

@@ -553,56 +553,9 @@ __device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav
 // for both; then each kind's tests run on their lanes.  The memory-latency-bound
 // global mode trades the second kind's idle lanes for half the round trips;
 // each lane's steps, and so its decisions, are unchanged.
-// Inline leaves (KParams::inline_leaves): when the expanded node's right child c1 is a leaf of one or
-// two triangles, its triangle records follow the child pair in the node array, and the fused step
-// that expands the parent reads them with the pair.  The reference visits c1 right after pushing c0,
-// so a c1 that passes its box is tested in the same step: one memory round trip fewer per such leaf,
-// the same decisions in the same order.
-#ifndef SRT_INLINE_LEAVES
-#define SRT_INLINE_LEAVES 1
-#endif
 template <bool COUNT, bool PACK, int RING = kShortStack, bool TL = false>
 __device__ __forceinline__ void trav_fused(const KParams& kp, const Lane& ln, Counters& c, Trav& t, bool any) {
   const bool at_int = t.cnt == 0u, at_leaf = trav_at_leaf(t.cnt) && !(TL && t.cnt == kTreeletCnt);
-#if SRT_INLINE_LEAVES
-  if (kp.inline_leaves && !TL) {
-    if (at_int | at_leaf) {
-      const uint32_t ref0 = t.ref | kp.ref_or;
-      const bool spine = kSpine<false> && at_int && (ref0 != t.ref);
-      // internal: the pair in x[0..3], then what follows it: c1's pair (spine) or c1's inline triangle
-      // records (else; meaningful only when c1 is a leaf of <= 2 triangles); leaf: its two records in x[4..9]
-      static_assert(kLeafTris == 2, "trav_fused loads two triangle records");
-      const float4* p = at_leaf ? kp.tris + 3 * (size_t)t.ref : kp.nodes + (2 * ref0 + 2);
-      const float4* q = at_leaf ? p : p + 4;
-      float4 x[10];
-      if (at_int) {
-        x[0] = p[0];
-        x[1] = p[1];
-        x[2] = p[2];
-        x[3] = p[3];
-      }
-      x[4] = q[0];
-      x[5] = q[1];
-      x[6] = q[2];
-      x[7] = q[3];
-      if (!spine) {
-        x[8] = q[4];
-        x[9] = q[5];
-      }
-      bool leaf_now = at_leaf;
-      if (at_int) {
-        trav_internal_x<COUNT, false, PACK, RING>(kp, ln, c, t, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], spine);
-        // c1 became current (its (first, count) -- or an identical leaf's, whose records are the same)
-        // and is a leaf of <= 2 triangles: its records are x[4..9]
-        leaf_now = !spine && (t.ref == __float_as_uint(x[2].w)) && (t.cnt == __float_as_uint(x[3].w)) &&
-                   (t.cnt - 1u < 2u);
-      }
-      if (leaf_now) trav_leaf_x<COUNT, false>(kp, c, t, any, x + 4);
-    }
-    trav_pop<false, PACK, RING>(kp, ln, t);
-    return;
-  }
-#endif
   if (at_int | at_leaf) {
     const uint32_t ref0 = t.ref | kp.ref_or;
     const bool spine = kSpine<false> && at_int && (ref0 != t.ref);

@@ -61,6 +61,9 @@ int main(int argc, char** argv) {
   f = std::fopen((out_prefix + ".rgba8").c_str(), "wb");
   if (!f || std::fwrite(out.data(), 1, out.size(), f) != out.size()) return 1;
   std::fclose(f);
-  std::printf("OK %s\n", rt.Transport());
+  const auto ms = rt.KernelMs();
+  for (float m : ms)
+    if (!(m > 0.0f)) return 2;  // every device ran its launch (HIP events around it)
+  std::printf("OK %s %d\n", rt.Transport(), rt.Ranks());
   return 0;
 }

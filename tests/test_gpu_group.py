@@ -89,6 +89,7 @@ def test_cpp_compute_group_main_loop(setup, want, tmp_path, devices):
     last = res.stdout.strip().splitlines()[-1] if res.stdout.strip() else ""  # (RCCL prints a banner first)
     assert res.returncode == 0 and last.startswith("OK"), res.stdout + res.stderr
     assert last.split()[1] == ("rccl" if len(set(devices)) == len(devices) else "copy")
+    assert int(last.split()[2]) == len(devices)  # the ranks RCCL sees (or the contexts, copy transport)
     acc = np.fromfile(tmp_path / "g.accum", np.float32).reshape(48, 64, 4)
     out = np.fromfile(tmp_path / "g.rgba8", np.uint8).reshape(48, 64, 4)
     assert bits_equal(acc, want[0]).all() and (out == want[1]).all()

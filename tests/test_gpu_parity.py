@@ -200,18 +200,9 @@ def test_synthetic_mesh_global_mode():
     assert_parity(setup, 2)
 
 
-@pytest.mark.parametrize("inline", ["1", "0"])
-def test_surface_mesh_global_mode(monkeypatch, inline):
-    """bench.py's surface_mesh leg: the 262k-triangle torus-knot tube (global-scene mode) against the oracle,
-    with and without inline leaves (the fused step tests a small right-child leaf from its parent's round
-    trip; chosen by default for fused-schedule scenes)."""
-    monkeypatch.setenv("SRT_INLINE_LEAVES", inline)
+def test_surface_mesh_global_mode():
+    """bench.py's surface_mesh leg: the 262k-triangle torus-knot tube (global-scene mode) against the oracle."""
     setup = R.make_setup(64, 40, show_model=True, models=[R.torus_knot_model()])
-    r = R.Renderer(setup)
-    try:
-        assert r.compute.GetInt("scene.inline_leaves") == int(inline)
-    finally:
-        r.close()
     assert_parity(setup, 2)
 
 
@@ -220,11 +211,7 @@ def test_surface_mesh_global_mode(monkeypatch, inline):
                                  {"SRT_NODE_ALIGN": "0", "SRT_GLOBAL_FUSED_MODE": "0"},
                                  {"SRT_NODE_LAYOUT": "0", "SRT_GLOBAL_FUSED_MODE": "1"},
                                  {"SRT_GLOBAL_WAVES_MODE": "4"},
-                                 {"SRT_NODE_ALIGN": "1", "SRT_GLOBAL_WAVES_MODE": "5"},
-                                 {"SRT_INLINE_LEAVES": "0"},
-                                 {"SRT_INLINE_LEAVES": "1", "SRT_NODE_ALIGN": "1", "SRT_GLOBAL_FUSED_MODE": "1"},
-                                 {"SRT_INLINE_LEAVES": "1", "SRT_GLOBAL_WAVES_MODE": "4"},
-                                 {"SRT_INLINE_LEAVES": "1", "SRT_GLOBAL_FUSED_MODE": "0"}])
+                                 {"SRT_NODE_ALIGN": "1", "SRT_GLOBAL_WAVES_MODE": "5"}])
 def test_node_layouts_global_mode(monkeypatch, env):
     """The device node layouts (pathtrace.hip LayoutNodes): line-aligned right-child chains (chosen for
     scenes past the Infinity Cache) and the reference's own order (no right-spine double steps) render
