@@ -331,12 +331,15 @@ class GroupRun:
         self.setup, self.spp = setup, spp
         self.devices = list(devices)
         self.grp = R.GroupRenderer(setup, self.devices, band_rows=band_rows)
+        self.enqueue_s = []
 
     def count(self) -> dict:
         return self.grp.count(self.spp)
 
     def step(self):
+        t0 = time.perf_counter()
         self.grp.render(self.spp)
+        self.enqueue_s.append(time.perf_counter() - t0)  # host time to enqueue every device's step
 
     def sync(self):
         self.grp.finish()
@@ -352,7 +355,8 @@ class GroupRun:
         return {"mode": "in-process device group (srt_group_*)", "transport": g.transport,
                 "rccl_ranks": g.get_int("ranks"), "contexts": g.get_int("contexts"), "devices": self.devices,
                 "gather_bytes_per_frame": g.get_int("bytes.output") * 1024,
-                "radiance_gathers_in_timed_steps": g.get_int("gathers.accum")}
+                "radiance_gathers_in_timed_steps": g.get_int("gathers.accum"),
+                "host_enqueue_ms_per_step": round(1e3 * float(np.median(self.enqueue_s)), 3) if self.enqueue_s else None}
 
     def close(self):
         self.grp.close()

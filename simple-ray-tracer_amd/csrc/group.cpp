@@ -20,10 +20,15 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "srt_internal.hpp"
@@ -73,9 +78,79 @@ const Rccl& rccl() {
   return r;
 }
 
+// One host thread per context beyond the first: every device's launches of a frame are enqueued at
+// once rather than one device after another (a launch costs tens of microseconds of host API calls,
+// so with 8 devices the last would start a good fraction of a millisecond after the first).
+// Run(job) calls job(i) for every context i, job(0) on the calling thread, and returns the first
+// non-zero status.  SRT_GROUP_THREADS=0 enqueues serially on the calling thread.
+class Workers {
+ public:
+  explicit Workers(int n) : rc_(n, 0) {
+    for (int i = 1; i < n; ++i) threads_.emplace_back([this, i] { Loop(i); });
+  }
+  ~Workers() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : threads_) t.join();
+  }
+  int Run(const std::function<int(int)>& job) {
+    const int n = (int)rc_.size();
+    if (threads_.empty()) {
+      for (int i = 0; i < n; ++i)
+        if (int rc = job(i)) return rc;
+      return 0;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &job;
+      pending_ = n - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    rc_[0] = job(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [this] { return pending_ == 0; });
+    job_ = nullptr;
+    for (int r : rc_)
+      if (r) return r;
+    return 0;
+  }
+
+ private:
+  void Loop(int i) {
+    long long seen = 0;
+    for (;;) {
+      const std::function<int(int)>* job = nullptr;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        job = job_;
+      }
+      const int r = (*job)(i);
+      std::lock_guard<std::mutex> lk(mu_);
+      rc_[i] = r;
+      if (--pending_ == 0) done_cv_.notify_one();
+    }
+  }
+  std::vector<std::thread> threads_;
+  std::vector<int> rc_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<int(int)>* job_ = nullptr;
+  long long gen_ = 0;
+  int pending_ = 0;
+  bool stop_ = false;
+};
+
 }  // namespace
 
 struct srt_group {
+  std::unique_ptr<Workers> workers;  // per-context launch threads
   std::vector<srt_context*> ctx;
   std::vector<int> dev;
   std::vector<hipStream_t> stream;  // each context's render stream (srt_stream)
@@ -178,15 +253,13 @@ int CreateStreamsEvents(srt_group* g) {
   return SRT_OK;
 }
 
-// Before a launch that writes sRGB8 buffer `b`: every context's image buffers point at its band
-// images, and its render stream waits for the gathers that last read them.
-int PrepareLaunch(srt_group* g, int b) {
-  for (size_t i = 0; i < g->ctx.size(); ++i) {
-    if (int rc = srt_set_image_buffers(g->ctx[i], g->band_accum[i], g->band_out[b][i])) return rc;
-    GHIP(hipSetDevice(g->dev[i]));
-    GHIP(hipStreamWaitEvent(g->stream[i], g->sent[b][i], 0));
-    GHIP(hipStreamWaitEvent(g->stream[i], g->acc_sent[i], 0));
-  }
+// Before a launch that writes sRGB8 buffer `b`: context i's image buffers point at its band images,
+// and its render stream waits for the gathers that last read them.
+int PrepareLaunch(srt_group* g, int i, int b) {
+  if (int rc = srt_set_image_buffers(g->ctx[i], g->band_accum[i], g->band_out[b][i])) return rc;
+  GHIP(hipSetDevice(g->dev[i]));
+  GHIP(hipStreamWaitEvent(g->stream[i], g->sent[b][i], 0));
+  GHIP(hipStreamWaitEvent(g->stream[i], g->acc_sent[i], 0));
   return SRT_OK;
 }
 
@@ -302,12 +375,15 @@ int srt_group_create(srt_context* const* ctxs, int n, int band_rows, srt_group**
     srt_group_destroy(g);
     return rc;
   }
+  const char* th = std::getenv("SRT_GROUP_THREADS");
+  g->workers = std::make_unique<Workers>((th && th[0] == '0') ? 1 : n);
   *out = g;
   return SRT_OK;
 }
 
 int srt_group_destroy(srt_group* g) {
   if (!g) return SRT_ERR_INVALID;
+  g->workers.reset();
   (void)srt_group_finish(g);
   // the contexts outlive the group: give each its own full-frame images back (and tiling 0 of 1), so
   // that no context keeps a pointer to the band images freed below
@@ -433,9 +509,12 @@ int srt_group_alloc_images(srt_group* g) {
 
 int srt_group_dispatch(srt_group* g, uint32_t gx, uint32_t gy) {
   if (!g || !g->recv_out) return SRT_ERR_STATE;
-  if (int rc = PrepareLaunch(g, g->cur)) return rc;
-  for (srt_context* c : g->ctx)
-    if (int rc = srt_dispatch(c, gx, gy)) return rc;
+  const int b = g->cur;
+  if (int rc = g->workers->Run([&](int i) {
+        if (int r = PrepareLaunch(g, i, b)) return r;
+        return srt_dispatch(g->ctx[i], gx, gy);
+      }))
+    return rc;
   g->accum_stale = true;
   int reset = 0;
   srt_get_int(g->ctx[0], "resetAccumBuffer", &reset);
@@ -451,9 +530,12 @@ int srt_group_render_frames(srt_group* g, int frame_first, int nframes) {
   if (!g || !g->recv_out) return SRT_ERR_STATE;
   if (nframes < 0 || frame_first < 1) return SRT_ERR_INVALID;
   if (nframes == 0) return SRT_OK;
-  if (int rc = PrepareLaunch(g, g->cur)) return rc;
-  for (srt_context* c : g->ctx)
-    if (int rc = srt_render_frames(c, frame_first, nframes, 1, 0)) return rc;
+  const int b = g->cur;
+  if (int rc = g->workers->Run([&](int i) {
+        if (int r = PrepareLaunch(g, i, b)) return r;
+        return srt_render_frames(g->ctx[i], frame_first, nframes, 1, 0);
+      }))
+    return rc;
   g->accum_stale = true;
   const int rc = GatherOutput(g, g->cur, g->W, g->H);
   g->cur ^= 1;

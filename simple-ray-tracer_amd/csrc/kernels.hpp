@@ -34,6 +34,9 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
 #ifndef SRT_TILE_SCHED
 #define SRT_TILE_SCHED 1  // tiles of each frame in the last launch's cost order
 #endif
+#ifndef SRT_NT_SAMPLES
+#define SRT_NT_SAMPLES 0  // sample-buffer stores with the streaming (nontemporal) policy
+#endif
 // The IL instance (trees past 600 MB) deals a tile's frames in a row (C5 783 -> 771 ms per launch,
 // A/B on one box; 8 or 16 batches per claim instead of 4: 776 / 792 ms)
 #ifndef SRT_TILE_MAJOR_IL
@@ -336,7 +339,14 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
       atomicAdd(&kp.tile_cost[(ly >> 3) * tiles_x + (px >> 3)], (uint32_t)(bounces + 1));
     }
     color = color + T * mk(0.05f, 0.05f, 0.05f);  // skyColor, raytrace_compute.glsl:219,292
+#if SRT_NT_SAMPLES
+    // streaming store: the sample buffer passes through L2 once, and would evict the noise tables
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f v = {color.x, color.y, color.z, 0.0f};
+    __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(kp.lbuf + ((size_t)fidx * (size_t)kp.local_pixels + (size_t)li)));
+#else
     kp.lbuf[(size_t)fidx * (size_t)kp.local_pixels + (size_t)li] = make_float4(color.x, color.y, color.z, 0.0f);
+#endif
     has_work = false;
   };
 

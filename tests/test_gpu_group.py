@@ -59,6 +59,15 @@ def test_group_per_frame_dispatch(setup, want):
     assert bits_equal(acc, want[0]).all() and (out == want[1]).all()
 
 
+def test_group_serial_enqueue(setup, want, monkeypatch):
+    """SRT_GROUP_THREADS=0: every context's launches enqueued from the calling thread (by default each
+    context beyond the first has a launch thread of its own); the same frame."""
+    monkeypatch.setenv("SRT_GROUP_THREADS", "0")
+    acc, out, transport = _group_frame(setup, [0, 0, 0], 2, per_frame=True)
+    assert transport == "copy"
+    assert bits_equal(acc, want[0]).all() and (out == want[1]).all()
+
+
 def test_group_forced_copy_transport(setup, want, monkeypatch):
     monkeypatch.setenv("SRT_GROUP_TRANSPORT", "copy")
     acc, out, transport = _group_frame(setup, [0], 8)

@@ -1,6 +1,7 @@
 #!/usr/bin/env python
-"""Reduces tools/c2_study.sh's runs (gpurun_out/c2s/b<N>/) into profiles/r04_c2_study.json: for each
-sphere_kernel occupancy (blocks per CU), the timed launch's kernel time and its counters, per launch.
+"""Reduces a counter study's runs into JSON: tools/c2_study.sh (gpurun_out/c2s/b<N>/, one per
+sphere_kernel occupancy) or tools/pmc_study.sh (gpurun_out/<name>/<variant>/, --kernel PREFIX): for each,
+the timed launch's kernel time and its counters, per launch.
 
   valu_issue      SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x kernel time x 2.4 GHz)
   lane_util       SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU)
@@ -10,6 +11,7 @@ sphere_kernel occupancy (blocks per CU), the timed launch's kernel time and its 
   fetch_lines_B   2 x FETCH_SIZE (128-B line requests tallied at 64 B on gfx950), per launch and per sample
   write_B         WRITE_SIZE, per launch and per sample (a sample's record is 16 B)
 usage: python tools/c2_study.py gpurun_out/c2s [--out profiles/r04_c2_study.json]
+       python tools/c2_study.py gpurun_out/torus --kernel "void srt::sample_kernel<false" --out ...
 """
 from __future__ import annotations
 
@@ -23,13 +25,13 @@ SIMDS = 1024
 KERNEL = "void srt::sphere_kernel<false>"
 
 
-def counters(d: pathlib.Path) -> dict:
+def counters(d: pathlib.Path, kernel: str = KERNEL) -> dict:
     out = {}
     for sub in ("pmc_sq", "pmc_sq2", "pmc_fetch", "pmc_write", "pmc_tcc", "pmc_tcp"):
         p = d / sub / "run_counter_collection.csv"
         if not p.exists():
             continue
-        rows = [r for r in csv.DictReader(open(p)) if r["Kernel_Name"].startswith(KERNEL)]
+        rows = [r for r in csv.DictReader(open(p)) if r["Kernel_Name"].startswith(kernel)]
         ids = sorted({int(r["Dispatch_Id"]) for r in rows})
         if not ids:
             continue
@@ -44,23 +46,32 @@ def main():
     root = pathlib.Path(sys.argv[1])
     outp = pathlib.Path(sys.argv[sys.argv.index("--out") + 1]) if "--out" in sys.argv else \
         pathlib.Path(__file__).resolve().parents[1] / "profiles" / "r04_c2_study.json"
-    res = {"workload": "spheres_1024x1024_64spp_depth4 (C2), sphere_kernel<false>, one timed launch per pass",
-           "by_blocks": {}}
-    for d in sorted(root.glob("b*")):
-        n = int(d.name[1:])
+    kernel = sys.argv[sys.argv.index("--kernel") + 1] if "--kernel" in sys.argv else KERNEL
+    study = "--kernel" in sys.argv
+    res = {"workload": "spheres_1024x1024_64spp_depth4 (C2), sphere_kernel<false>, one timed launch per pass"
+           if not study else f"{root.name}: {kernel}..., one timed launch per pass", "by_blocks": {}}
+    for d in sorted(p for p in root.iterdir() if p.is_dir()):
+        n = d.name[1:] if not study else d.name
         bench = json.loads((d / "bench.json").read_text())
         k_ms = bench["roofline"]["kernel_ms"]
-        c = counters(d)
-        samples = 1024 * 1024 * 64
-        e = {"blocks_per_cu": n, "waves_per_simd": n, "kernel_ms": k_ms, "Mrays_s": bench["value"],
+        c = counters(d, kernel)
+        cfg = bench["config"]
+        samples = cfg["width"] * cfg["height"] * cfg["spp"]
+        e = {"variant": n, "kernel_ms": k_ms, "Mrays_s": bench["value"], "rays": bench["rays_per_step"],
              "code_hash": bench["code_hash"], "counters": c}
         ks = k_ms * 1e-3
         if "SQ_INSTS_VALU" in c:
             e["valu_issue"] = c["SQ_INSTS_VALU"] * 2 / (SIMDS * ks * CLOCK)
             e["lane_util"] = c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_INSTS_VALU"])
             e["wait_any"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
-        if "SQ_WAIT_INST_ANY" in c:
-            e["wait_inst"] = c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"] if "SQ_WAVE_CYCLES" in c else None
+        if "SQ_WAIT_INST_ANY" in c and "SQ_WAVE_CYCLES" in c:
+            e["wait_inst"] = c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"]
+            e["active_inst"] = c["SQ_ACTIVE_INST_ANY"] / c["SQ_WAVE_CYCLES"] if "SQ_ACTIVE_INST_ANY" in c else None
+        for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS"):
+            if k in c:
+                e[k.lower() + "_per_ray"] = c[k] / bench["rays_per_step"]
+        if "TCP_TOTAL_CACHE_ACCESSES_sum" in c:
+            e["l1_miss_req_frac"] = c["TCP_TCC_READ_REQ_sum"] / max(c["TCP_TOTAL_CACHE_ACCESSES_sum"], 1.0)
         if "TCC_HIT_sum" in c:
             e["l2_hit"] = c["TCC_HIT_sum"] / max(c["TCC_HIT_sum"] + c["TCC_MISS_sum"], 1.0)
         if "FETCH_SIZE" in c:
@@ -71,8 +82,9 @@ def main():
             e["write_B_per_sample"] = e["write_B"] / samples
         res["by_blocks"][str(n)] = e
     outp.write_text(json.dumps(res, indent=1) + "\n")
-    keys = ("kernel_ms", "valu_issue", "lane_util", "wait_any", "wait_inst", "l2_hit", "fetch_lines_B_per_sample",
-            "write_B_per_sample")
+    keys = ("kernel_ms", "valu_issue", "lane_util", "wait_any", "wait_inst", "active_inst", "l2_hit",
+            "l1_miss_req_frac", "fetch_lines_B_per_sample", "write_B_per_sample", "sq_insts_valu_per_ray",
+            "sq_insts_salu_per_ray", "sq_insts_vmem_rd_per_ray", "sq_insts_lds_per_ray")
     print("blocks " + " ".join(keys))
     for n, e in res["by_blocks"].items():
         print(n, " ".join(f"{e.get(k, float('nan')):.4g}" if isinstance(e.get(k), (int, float)) else "-" for k in keys))

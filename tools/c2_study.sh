@@ -12,7 +12,7 @@ for n in ${BLOCKS:-3 4 5 6}; do
     --width 1024 --height 1024 --spp 64 --max-depth 4 > $O/bench.json 2> $O/bench.err || exit 1
   timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT \
     SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_SALU --output-format csv -d $O/pmc_sq -o run -- $B > $O/pmc_sq.log 2>&1 || exit 1
-  timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_WAVES GRBM_GUI_ACTIVE \
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE \
     --output-format csv -d $O/pmc_sq2 -o run -- $B > $O/pmc_sq2.log 2>&1 || exit 1
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- $B > $O/pmc_fetch.log 2>&1 || exit 1
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- $B > $O/pmc_write.log 2>&1 || exit 1
