@@ -85,8 +85,9 @@ const Rccl& rccl() {
 // non-zero status.  SRT_GROUP_THREADS=0 enqueues serially on the calling thread.
 class Workers {
  public:
-  explicit Workers(int n) : rc_(n, 0) {
-    for (int i = 1; i < n; ++i) threads_.emplace_back([this, i] { Loop(i); });
+  Workers(int n, bool threads) : rc_(n, 0) {
+    if (threads)
+      for (int i = 1; i < n; ++i) threads_.emplace_back([this, i] { Loop(i); });
   }
   ~Workers() {
     {
@@ -376,7 +377,7 @@ int srt_group_create(srt_context* const* ctxs, int n, int band_rows, srt_group**
     return rc;
   }
   const char* th = std::getenv("SRT_GROUP_THREADS");
-  g->workers = std::make_unique<Workers>((th && th[0] == '0') ? 1 : n);
+  g->workers = std::make_unique<Workers>(n, !(th && th[0] == '0'));
   *out = g;
   return SRT_OK;
 }
