@@ -34,6 +34,10 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
 #ifndef SRT_TILE_SCHED
 #define SRT_TILE_SCHED 1  // tiles of each frame in the last launch's cost order
 #endif
+// sphere_kernel: trace a bounce's shadow ray in the shading pass that set it up (one sphere test)
+#ifndef SRT_SPH_SHADOW_NOW
+#define SRT_SPH_SHADOW_NOW 1
+#endif
 #ifndef SRT_NT_SAMPLES
 #define SRT_NT_SAMPLES 0  // sample-buffer stores with the streaming (nontemporal) policy
 #endif
@@ -138,22 +142,23 @@ __device__ __forceinline__ int shade_hit(const KParams& kp, const Lane& ln, Coun
     // otherwise costs n - 1 dependent gathers, and with ~35 shading lanes
     // nearly every wave has such a lane.
     float total = ris, pdf = 0.0f;  // 0 + ris
-    if (u_sel0 < (ris / total)) {
+    const float sel0 = div_rn(ris, total);
+    if (u_sel0 < sel0) {
       pdf = lpdf;
       selected = true;
     }
-    const bool draws = !selected && (ris / total == ris / total);
+    const bool draws = !selected && (sel0 == sel0);
     for (int i = 1; i < n; ++i) {
       total += ris;
       if (draws && !selected) {
         const float r = randU<COUNT>(kp, ln, c, p.y + (float)i, p.z + (float)i);
-        if (r < (ris / total)) {
+        if (r < div_rn(ris, total)) {
           pdf = lpdf;
           selected = true;
         }
       }
     }
-    lw = (total / (float)n) / fmx(0.001f, pdf);
+    lw = div_rn(div_rn(total, (float)n), fmx(0.001f, pdf));
   }
 
   // ---- direct light, both shadow outcomes (raytrace_compute.glsl:233-246) ----
@@ -506,6 +511,25 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
         } else {
           shadow_phase = next == kShadeShadow;
           pending = true;  // started with the refill's new rays (one start_ray pass)
+          if constexpr (SPH && SRT_SPH_SHADOW_NOW) {
+            // The sphere scene's shadow ray is one test of the five spheres: it is traced here, in
+            // the iteration that set it up, rather than in the next one -- the same test and the
+            // same colour addition, in the path's order (as in the shadow_phase branch above) --
+            // so each iteration moves every hit lane one whole bounce and more lanes shade together.
+            if (shadow_phase) {
+              pending = false;
+              start_ray();
+              color = color + ((hit_sphere >= 0) ? q0 : q1);
+              if (term) {
+                finish_sample();
+              } else {
+                rd = nd;
+                tmax = __builtin_inff();
+                shadow_phase = false;
+                pending = true;
+              }
+            }
+          }
         }
       }
     }

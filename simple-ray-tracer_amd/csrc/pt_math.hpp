@@ -39,13 +39,39 @@ __device__ __forceinline__ float recip_exact(float b) {
   return r;
 }
 
+// ---- correctly rounded division ---------------------------------------------
+// a / b, correctly rounded (the contract's '/').  SRT_FAST_DIV: the verified Newton reciprocal r of
+// b, q = a * r, and one Markstein correction q + (a - b*q) * r with the residual exact in an FMA;
+// equal to the IEEE quotient for every a, b inside the range checked below (2^-62 <= |a|, |b| <= 2^62,
+// or a == 0: no intermediate over- or underflows, so the result is the same for every exponent
+// pair), all 2^46 mantissa pairs checked on gfx950 (tools/div_exhaustive.hip); other inputs take
+// the division on a branch that is skipped unless some lane needs it.  An exact quotient (zero
+// residual) is q itself, which keeps the sign of a zero quotient.
+#ifndef SRT_FAST_DIV
+#define SRT_FAST_DIV 0
+#endif
+__device__ __forceinline__ float div_rn(float a, float b) {
+#if SRT_FAST_DIV
+  const float r = recip_newton(b);
+  const float q = a * r;
+  const float e = __builtin_fmaf(-b, q, a);
+  float res = (e == 0.0f) ? q : __builtin_fmaf(e, r, q);
+  const float ma = __builtin_fabsf(a), mb = __builtin_fabsf(b);
+  const bool ok = (ma <= 0x1p62f) & ((ma >= 0x1p-62f) | (a == 0.0f)) & (mb >= 0x1p-62f) & (mb <= 0x1p62f);
+  if (__builtin_expect(!ok, 0)) res = a / b;
+  return res;
+#else
+  return a / b;
+#endif
+}
+
 __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
 __device__ __forceinline__ f3 operator+(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ f3 operator-(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 __device__ __forceinline__ f3 operator*(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
 __device__ __forceinline__ f3 operator*(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
 __device__ __forceinline__ f3 operator*(float s, f3 a) { return mk(s * a.x, s * a.y, s * a.z); }
-__device__ __forceinline__ f3 operator/(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ f3 operator/(f3 a, float s) { return mk(div_rn(a.x, s), div_rn(a.y, s), div_rn(a.z, s)); }
 __device__ __forceinline__ f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
 // GLSL dot / cross built-ins with fused multiply-adds, as GPU compilers evaluate
 // them: dot = fma(z, z', fma(y, y', x * x')),

@@ -75,9 +75,9 @@ __device__ __forceinline__ bool sphere_hit(f3 ro, f3 rd, f3 pos, float radius, f
   const float disc = h * h - a * cc;
   if (disc < 0.0f) return false;
   const float sq = __builtin_sqrtf(disc);
-  float root = (h - sq) / a;
+  float root = div_rn(h - sq, a);
   if (!(mn < root && root < mx)) {
-    root = (h + sq) / a;
+    root = div_rn(h + sq, a);
     if (!(mn < root && root < mx)) return false;
   }
   t = root;
@@ -119,20 +119,20 @@ __device__ __forceinline__ LightRec load_light(const KParams& kp, Counters& c, i
 __device__ __forceinline__ float ggxD(float NdotH, float rough) {
   const float a2 = rough * rough;
   const float d = ((NdotH * a2 - NdotH) * NdotH + 1.0f);
-  return a2 / fmx(0.001f, (d * d * 3.1415926535897f));
+  return div_rn(a2, fmx(0.001f, (d * d * 3.1415926535897f)));
 }
 __device__ __forceinline__ float ggxDNew(float NdotH, float alphaSquared) {
   const float b = ((alphaSquared - 1.0f) * NdotH * NdotH + 1.0f);
-  return alphaSquared / fmx(0.001f, (3.1415926535897f * b * b));
+  return div_rn(alphaSquared, fmx(0.001f, (3.1415926535897f * b * b)));
 }
 __device__ __forceinline__ float ggxSchlickMasking(float NdotL, float NdotV, float rough) {
   const float k = rough * rough / 2.0f;
-  const float gv = NdotV / fmx(0.001f, (NdotV * (1.0f - k) + k));
-  const float gl = NdotL / fmx(0.001f, (NdotL * (1.0f - k) + k));
+  const float gv = div_rn(NdotV, fmx(0.001f, (NdotV * (1.0f - k) + k)));
+  const float gl = div_rn(NdotL, fmx(0.001f, (NdotL * (1.0f - k) + k)));
   return __builtin_fabsf(gv * gl);
 }
 __device__ __forceinline__ float smithGAlpha(float alpha, float NdotS) {
-  return NdotS / (fmx(0.0001f, alpha) * __builtin_sqrtf(1.0f - fmn(0.99999f, NdotS * NdotS)));
+  return div_rn(NdotS, fmx(0.0001f, alpha) * __builtin_sqrtf(1.0f - fmn(0.99999f, NdotS * NdotS)));
 }
 __device__ __forceinline__ float smithLambda(float a) {
   return (-1.0f + __builtin_sqrtf(1.0f + recip_exact(fmx(0.001f, a * a)))) * 0.5f;
@@ -192,7 +192,7 @@ __device__ float brdf_probability(const Mat& m, f3 Vv, f3 N) {
   const f3 f0 = mk(sF0, sF0, sF0);
   const float F = sat(luminance(fresnelSchlickNew(f0, shadowedF90(f0), fmx(0.0f, dot(Vv, N)))));
   const float diffuse = dR * (1.0f - F);
-  const float p = (F / fmx(0.0001f, (F + diffuse)));
+  const float p = div_rn(F, fmx(0.0001f, (F + diffuse)));
   return clampf(p, 0.1f, 0.9f);
 }
 
@@ -201,7 +201,7 @@ __device__ __forceinline__ f3 specular_half(float rx, float ry, float rough, f3 
   const f3 B = perpendicular(N);
   const f3 T = cross(B, N);
   const float a2 = rough * rough;
-  const float cosT = __builtin_sqrtf(fmx(0.0f, (1.0f - rx) / ((a2 - 1.0f) * rx + 1.0f)));
+  const float cosT = __builtin_sqrtf(fmx(0.0f, div_rn(1.0f - rx, (a2 - 1.0f) * rx + 1.0f)));
   const float sinT = __builtin_sqrtf(fmx(0.0f, 1.0f - cosT * cosT));
   const float phi = ry * 3.1415926535897f * 2.0f;
   return ((T * (sinT * cos_f(phi))) + (B * (sinT * sin_f(phi)))) + (N * cosT);
@@ -231,7 +231,7 @@ __device__ bool sample_indirect(const Hit& hit, f3 Vv, int type, float r1, float
   const float cphi = cos_f(phi), sphi = sin_f(phi);
   // SampleSpecularHalfVec(r1, r2, roughness, N) (brdf.glsl:81-99)
   const float a2 = hit.mat.roughness * hit.mat.roughness;
-  const float cosT = __builtin_sqrtf(fmx(0.0f, (1.0f - r1) / ((a2 - 1.0f) * r1 + 1.0f)));
+  const float cosT = __builtin_sqrtf(fmx(0.0f, div_rn(1.0f - r1, (a2 - 1.0f) * r1 + 1.0f)));
   const float sinT = __builtin_sqrtf(fmx(0.0f, 1.0f - cosT * cosT));
   const f3 Hs = ((T * (sinT * cphi)) + (B * (sinT * sphi))) + (N * cosT);
   f3 nd, w0;
@@ -255,7 +255,7 @@ __device__ bool sample_indirect(const Hit& hit, f3 Vv, int type, float r1, float
     fx = fmx(0.00001f, fmn(1.0f, dot(H, L)));  // HdotL
     const float NdotL = fmx(0.00001f, fmn(1.0f, dot(N, L)));
     const float N2 = NdotL * NdotL;
-    w0 = mk(2.0f / (__builtin_sqrtf(((alphaSq * (1.0f - N2)) + N2) / N2) + 1.0f), 0.0f, 0.0f);
+    w0 = mk(div_rn(2.0f, __builtin_sqrtf(div_rn((alphaSq * (1.0f - N2)) + N2, N2)) + 1.0f), 0.0f, 0.0f);
     nd = L;
   }
   const f3 F = fresnelSchlickNew(specF0, shadowedF90(specF0), fx);
