@@ -34,9 +34,10 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
 #ifndef SRT_TILE_SCHED
 #define SRT_TILE_SCHED 1  // tiles of each frame in the last launch's cost order
 #endif
-// sphere_kernel: trace a bounce's shadow ray in the shading pass that set it up (one sphere test)
+// sphere_kernel: trace a bounce's shadow ray (1), and its next ray too (2), in the shading pass that
+// set them up (each is one test of the five spheres)
 #ifndef SRT_SPH_SHADOW_NOW
-#define SRT_SPH_SHADOW_NOW 1
+#define SRT_SPH_SHADOW_NOW 2
 #endif
 #ifndef SRT_NT_SAMPLES
 #define SRT_NT_SAMPLES 0  // sample-buffer stores with the streaming (nontemporal) policy
@@ -511,11 +512,12 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
         } else {
           shadow_phase = next == kShadeShadow;
           pending = true;  // started with the refill's new rays (one start_ray pass)
-          if constexpr (SPH && SRT_SPH_SHADOW_NOW) {
-            // The sphere scene's shadow ray is one test of the five spheres: it is traced here, in
-            // the iteration that set it up, rather than in the next one -- the same test and the
-            // same colour addition, in the path's order (as in the shadow_phase branch above) --
-            // so each iteration moves every hit lane one whole bounce and more lanes shade together.
+          if constexpr (SPH && SRT_SPH_SHADOW_NOW >= 1) {
+            // The sphere scene's rays are one test of the five spheres each: the shadow ray is traced
+            // here, in the iteration that set it up, rather than in the next one -- the same test and
+            // the same colour addition, in the path's order (as in the shadow_phase branch above) --
+            // and (level 2) so is the bounce ray: a miss ends the sample now, a hit is shaded in the
+            // next iteration.  So every lane with a hit shades in every iteration.
             if (shadow_phase) {
               pending = false;
               start_ray();
@@ -528,6 +530,11 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
                 shadow_phase = false;
                 pending = true;
               }
+            }
+            if (SRT_SPH_SHADOW_NOW >= 2 && pending) {  // the bounce ray (kShadeBounce, or after the shadow ray)
+              pending = false;
+              start_ray();
+              if (hit_sphere < 0) finish_sample();  // else its hit is shaded in the next iteration's pass
             }
           }
         }
