@@ -92,6 +92,8 @@ def parse(argv=None):
     ap.add_argument("--surface-spp", type=int, default=64)
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (multi-rank tests on one GPU)")
+    ap.add_argument("--group", action="store_true",
+                    help="run the in-process device group even at --gpus 1 (one RCCL rank: the N > 1 path's code)")
     ap.add_argument("--dump", default=None, help="rank 0 saves the assembled frame (npz) after the last step")
     return ap.parse_args(argv)
 
@@ -441,7 +443,7 @@ def run_compute(run):
 
 
 def parallelism(args, mode, world, run) -> str:
-    if world == 1:
+    if world == 1 and mode != "group":
         return "single GPU"
     if mode == "group":
         return (f"row-band tiling x{world} ({args.band_rows}-row bands) over the devices of one process + per-frame "
@@ -462,7 +464,7 @@ def main(argv=None):
         if world_env != args.gpus:
             raise SystemExit(f"--gpus {args.gpus} differs from WORLD_SIZE {world_env}")
         mode, world = "dist", world_env  # torch.distributed.run: one rank per GPU
-    elif args.gpus > 1:
+    elif args.gpus > 1 or args.group:
         mode, world = "group", args.gpus  # plain `python bench.py --gpus N`: the in-process device group
         if not args.same_device and torch.cuda.device_count() < args.gpus:
             raise SystemExit(f"--gpus {args.gpus}: only {torch.cuda.device_count()} devices visible")

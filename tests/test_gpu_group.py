@@ -195,7 +195,8 @@ def test_group_destroy_gives_contexts_their_images_back(setup, want):
 def test_bench_in_process_group_same_device(tmp_path):
     """`python bench.py --gpus 4 --same-device` without torch.distributed: the in-process device group
     (four contexts on GPU 0, device-copy transport) renders the one-GPU frame bit for bit, and the line
-    names the transport, the ranks and every rank's kernel time."""
+    names the transport, the ranks and every rank's kernel time; `--gpus 1 --group` runs the group with
+    one RCCL rank (ncclCommInitAll, ncclGather) and renders the same frame."""
     import json
     import subprocess
     import sys
@@ -207,11 +208,11 @@ def test_bench_in_process_group_same_device(tmp_path):
     W, H, SPP = 96, 61, 3
     frames = {}
     lines = {}
-    for n in (1, 4):
+    for n, extra in ((1, []), (4, ["--same-device"]), ("1g", ["--group"])):
         dump = tmp_path / f"f{n}.npz"
-        cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--steps", "2", "--warmup", "1",
+        cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(n)[0], "--steps", "2", "--warmup", "1",
                "--width", str(W), "--height", str(H), "--spp", str(SPP), "--band-rows", "2", "--no-cpu-baseline",
-               "--no-global-leg", "--no-surface-leg", "--same-device", "--dump", str(dump)]
+               "--no-global-leg", "--no-surface-leg", "--dump", str(dump)] + extra
         env = {k: v for k, v in __import__("os").environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
         res = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=env)
         assert res.returncode == 0, res.stderr[-3000:]
@@ -224,3 +225,7 @@ def test_bench_in_process_group_same_device(tmp_path):
     assert j["group"]["transport"] == "copy" and j["group"]["rccl_ranks"] == 4 and j["group"]["contexts"] == 4
     assert len(j["kernel_ms_per_rank"]) == 4 and all(v > 0 for v in j["kernel_ms_per_rank"])
     assert j["group"]["radiance_gathers_in_timed_steps"] == 0
+    # --gpus 1 --group: the same in-process path with one RCCL rank (what N > 1 runs on distinct devices)
+    g = lines["1g"]
+    assert g["group"]["transport"] == "rccl" and g["group"]["rccl_ranks"] == 1
+    assert bits_equal(frames["1g"][0], frames[1][0]).all() and (frames["1g"][1] == frames[1][1]).all()
