@@ -298,12 +298,14 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
   // draining several expensive batches each (tools/wave_trace.py).
   // `batch` and everything derived from it are wave-uniform (scalar
   // registers); the counter's overshoot past n_batches stays below 2^31.
+  // The sphere scene's batches are cheap and take kClaimSph per claim.
+  constexpr int kC = SPH ? kClaimSph : kClaim;
   uint32_t claimed = 0;
-  int claim_sz = kp.tail_start > 0 ? kClaim : 1;  // size of the claim in flight
+  int claim_sz = kp.tail_start > 0 ? kC : 1;  // size of the claim in flight
   if (lane == 0) claimed = atomicAdd(kp.batch_ctr, (uint32_t)claim_sz);
   int batch = __builtin_amdgcn_readfirstlane((int)__shfl(claimed, 0));
   int claim_left = claim_sz - 1;  // batches of the current claim after `batch`
-  claim_sz = batch < kp.tail_start ? kClaim : 1;
+  claim_sz = batch < kp.tail_start ? kC : 1;
   if (lane == 0) claimed = atomicAdd(kp.batch_ctr, (uint32_t)claim_sz);
   int batch_next = 0;         // items of `batch` already handed out
 
@@ -422,7 +424,7 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
         } else {
           batch = __builtin_amdgcn_readfirstlane((int)__shfl(claimed, 0));
           claim_left = claim_sz - 1;
-          claim_sz = batch < kp.tail_start ? kClaim : 1;
+          claim_sz = batch < kp.tail_start ? kC : 1;
           if (lane == 0) claimed = atomicAdd(kp.batch_ctr, (uint32_t)claim_sz);
         }
         batch_next = 0;

@@ -133,6 +133,8 @@ struct srt_context {
   size_t lbuf_bytes = 0;
   size_t lbuf_cap = (size_t)16 << 30;  // SRT_SAMPLE_BUFFER_MB
   int tail_claims = 16;  // SRT_TAIL_CLAIMS: claims per wave before the end from which claims take one batch
+  int tail_claims_sph = 1;  // the sphere launch's (C2, 8 per claim: tail 16 6.20 ms, 1 3.17 ms; its batches
+                            // are cheap, the counter's atomic rate bounds it); SRT_TAIL_CLAIMS sets both
   int trav_frac16 = 9;                 // SRT_TRAV_FRAC16 (measured best on Rubik 1080p with the 16-sub-step pattern)
   int bounce_cap = 1 << 20;            // SRT_BOUNCE_CAP: bounces after which a path is cut (counted)
   int trav_frac16_global = 9;          // SRT_TRAV_FRAC16_GLOBAL: the same threshold for global-scene mode
@@ -456,7 +458,7 @@ int LaunchSpheres(srt_context* c, srt::KParams kp, size_t lds) {
   {
     const long long waves = (long long)blocks * 4;
     const long long n_batches = (long long)((kp.W + 7) >> 3) * ((kp.local_rows + 7) >> 3) * kp.nframes;
-    kp.tail_start = (int)std::max<long long>(0, n_batches - (long long)c->tail_claims * srt::kClaim * waves);
+    kp.tail_start = (int)std::max<long long>(0, n_batches - (long long)c->tail_claims_sph * srt::kClaimSph * waves);
   }
   HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
   hipLaunchKernelGGL(srt::sphere_kernel<COUNT>, dim3(blocks), dim3(256), lds, c->stream, kp);
@@ -797,7 +799,7 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   const size_t per_frame = (size_t)npx * sizeof(float4);
   // frames per launch: what the sample buffer holds, and n_tiles * frames < 2^31 (the kernel's batch index)
   const size_t n_tiles = (size_t)((kp.W + 7) >> 3) * (size_t)((kp.local_rows + 7) >> 3);
-  // (less 2^20: the batch counter overshoots the end by up to (kClaim + 1) claims per wave)
+  // (less 2^20: the batch counter overshoots the end by up to (max(kClaim, kClaimSph) + 1) claims per wave)
   // wavefront mode (global-scene, timed launches): its sample items (64 per batch) < 2^31 per chunk
   const bool wf = !ldsm && !count && kp.show_model && (c->wavefront >= 0 ? c->wavefront == 1 : c->wf_scene);
   const size_t max_frames = std::max<size_t>(
@@ -1112,7 +1114,7 @@ int srt_create(int device, void* stream, srt_context** out) {
   if (const char* e = std::getenv("SRT_WF_WAVES")) c->wf_waves = std::atoi(e);
   if (const char* e = std::getenv("SRT_TREELETS")) c->treelets = e[0] == '1' ? 1 : 0;
   if (const char* e = std::getenv("SRT_TREELET_DEPTH")) c->treelet_depth = std::max(0, std::min(srt::kTopStack - 1, std::atoi(e)));
-  if (const char* e = std::getenv("SRT_TAIL_CLAIMS")) c->tail_claims = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("SRT_TAIL_CLAIMS")) c->tail_claims = c->tail_claims_sph = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("SRT_TILE_ORDER")) c->tile_schedule = e[0] != '0';
   if (const char* e = std::getenv("SRT_TRAV_FRAC16")) c->trav_frac16 = std::max(0, std::min(16, std::atoi(e)));
   if (const char* e = std::getenv("SRT_TRAV_FRAC16_GLOBAL"))

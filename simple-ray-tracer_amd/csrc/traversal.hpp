@@ -369,6 +369,13 @@ constexpr int kShortStack = SRT_SHORT_STACK;
 #define SRT_CLAIM 4
 #endif
 constexpr int kClaim = SRT_CLAIM;
+// sphere_kernel: batches per claim (its batches are cheap: the launch counter's atomic rate, ~88 M claims/s,
+// not the tail, limits it; C2 on one box, kernel ms, with a tail window of 1 claim per wave: 4 per claim
+// 3.45, 8 3.17, 16 3.47; profiles/r04_experiments/claim_contention.txt)
+#ifndef SRT_CLAIM_SPH
+#define SRT_CLAIM_SPH 8
+#endif
+constexpr int kClaimSph = SRT_CLAIM_SPH;
 static_assert((kShortStack & (kShortStack - 1)) == 0, "kShortStack must be a power of two");
 constexpr int kTriPad = 3;                // zero records past the triangle array (>= kLeafTris - 1)
 constexpr uint32_t kNodePad = 2;          // zero node records past the array: the speculative next-pair read
