@@ -584,8 +584,11 @@ __global__ __launch_bounds__(BLOCK, LDSM ? 4 : GW) void sample_kernel(KParams kp
 
 // The sphere scene (SHOW_MODEL 0, raytrace_compute.glsl:299-364): the same loop, each ray testing the
 // five spheres in one go.
+#ifndef SRT_SPH_WAVES
+#define SRT_SPH_WAVES 4  // the register bound's waves per SIMD (it takes 87 VGPRs: 5 waves fit)
+#endif
 template <bool COUNT>
-__global__ __launch_bounds__(256, 4) void sphere_kernel(KParams kp) {
+__global__ __launch_bounds__(256, SRT_SPH_WAVES) void sphere_kernel(KParams kp) {
   sample_body<COUNT, false, true, 256, false, false, 4, true>(kp);
 }
 

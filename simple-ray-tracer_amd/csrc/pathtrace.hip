@@ -146,7 +146,7 @@ struct srt_context {
   int pool_slots_max = 4096;           // SRT_POOL_SLOTS: at most this many records
   int pool_deadline_ms = 30000;        // SRT_POOL_DEADLINE_MS: pool_kernel's watchdog
   int num_cus = 256;
-  int sphere_blocks = 3;               // SRT_SPHERE_BLOCKS: sphere_kernel blocks per CU
+  int sphere_blocks = 5;               // SRT_SPHERE_BLOCKS: sphere_kernel blocks per CU (at most)
   // wavefront mode (wavefront.hpp): global-scene launches through wf_logic / wf_shade / wf_trace
   int wavefront = -1;                  // SRT_WAVEFRONT=1/0 forces it on / off; -1: by scene (wf_scene)
   bool wf_scene = false;               // chosen at upload
@@ -452,8 +452,8 @@ int LaunchSpheres(srt_context* c, srt::KParams kp, size_t lds) {
     per_cu = std::max(per_cu, 1);
     c->occupancy.push_back({fn, lds, per_cu});
   }
-  // resident blocks per CU: the sphere loop runs best at 3 waves per SIMD (C2 on one box, ms per launch:
-  // 3 blocks 5.75, 4 5.88, 5 6.19, 6 6.24; its 87 VGPRs would allow 5); SRT_SPHERE_BLOCKS sets it
+  // resident blocks per CU: as many as its registers allow (C2 on one box, ms per launch: 3 blocks 3.23,
+  // 4 3.00, 5 2.93; while the launch counter's atomic rate bound it, round 3, 3 were best)
   const int blocks = c->num_cus * std::min(per_cu, c->sphere_blocks);
   {
     const long long waves = (long long)blocks * 4;
