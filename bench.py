@@ -431,7 +431,7 @@ def timed_kernel(c, scene: str) -> str:
     if scene == "rubik":
         return KERNEL_LDS
     if scene == "spheres":
-        return "srt::sphere_kernel<false> (spheres: no BVH, 3 waves per SIMD)"
+        return "srt::sphere_kernel<false> (spheres: no BVH, 5 waves per SIMD)"
     fused = c.GetInt("scene.fused") == 1
     gw = c.GetInt("scene.global_waves") if fused else 4
     return (f"srt::sample_kernel<false, false, true, 256, false, {'true' if fused else 'false'}, {gw}> "
