@@ -158,7 +158,7 @@ def code_hash() -> str:
 
 
 def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str, global_mode: bool = False) -> dict:
-    """Roofs of the dominant kernel, fractions of the live kernel time (HIP events on the launch stream):
+    """Roofs of the dominant kernel, fractions of the live kernel time (each launch's span on the GPU clock, srt_kernel_time):
     VALU issue (SQ_INSTS_VALU x 2 cycles per SIMD-32 over 1024 SIMDs), LDS-array cycles
     (SQ_LDS_IDX_ACTIVE over 256 CUs), HBM (corrected FETCH_SIZE + WRITE_SIZE over 8 TB/s).  The counters
     are per launch of this workload, from profiles/counters.json, and count only when they were collected
@@ -291,7 +291,10 @@ class RankRun:
         torch.cuda.synchronize(self.dev)
 
     def kernel_ms(self) -> list:
-        return [self.c.last_kernel_ms()]  # HIP events around sample_kernel on the launch stream
+        return [self.c.last_kernel_ms()]  # the last render's sample launches (their spans on the GPU clock)
+
+    def kernel_time(self) -> tuple:
+        return self.c.kernel_time()  # (summed ms, launches) since the previous call
 
     def frame(self):
         """Rank 0's frame after a step: (accum (H, W, 4) float32, sRGB8 (H, W, 4) uint8) on the host; None
@@ -388,16 +391,26 @@ def run_leg(setup, spp, args, *, mode, rank, world, device, stream):
     if mode == "dist" and world > 1:
         dist.barrier()
     run.sync()
+    # RankRun's steps are enqueued back to back (its sample launches are pipelined, DESIGN.md section 5:
+    # launch k+1 fills the CUs launch k's last waves leave idle); their kernel time is read once, after
+    # the timed region, from the launches' own spans.  The in-process group synchronises every step.
+    per_step_sync = mode == "group"
     kernel_ms = []
+    if not per_step_sync:
+        run.kernel_time()  # drops the counting and warmup launches
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run.step()
-        run.sync()
-        kernel_ms.append(run.kernel_ms())
+        if per_step_sync:
+            run.sync()
+            kernel_ms.append(run.kernel_ms())
     run.sync()
     if mode == "dist" and world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    if not per_step_sync:
+        total_ms, _launches = run.kernel_time()
+        kernel_ms = [[total_ms / args.steps]] * args.steps  # per step (one launch per step unless chunked)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64)
     if mode == "dist" and world > 1:
         elapsed = elapsed.to(run.dev) if args.backend == "nccl" else elapsed

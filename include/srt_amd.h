@@ -122,9 +122,16 @@ int srt_finish(srt_context* ctx);
  * uniform at frame_first + nframes - 1, as the last dispatch would. */
 int srt_render_frames(srt_context* ctx, int frame_first, int nframes, int write_output, int count);
 int srt_get_stats(srt_context* ctx, srt_stats* out);
-/* Device time of the path-tracing kernel launches of the last render call
- * (HIP events on the context's stream around each sample_kernel launch). */
+/* Device time of the path-tracing kernel launches of the last render call:
+ * each sample_kernel / sphere_kernel launch's span from its first wave's start
+ * to its last wave's end (the GPU's 100 MHz real-time clock; a pipelined launch
+ * overlaps its neighbours, which HIP events around it would count), and HIP
+ * events around pool and wavefront launches.  Waits for the render. */
 int srt_last_kernel_ms(srt_context* ctx, float* ms);
+/* The summed spans of every sample_kernel / sphere_kernel launch since the
+ * previous call (at most the last 1024), and how many: a timed loop of renders
+ * enqueued without synchronising reads its kernel time once.  Waits for them. */
+int srt_kernel_time(srt_context* ctx, double* total_ms, int* launches);
 int srt_reset_stats(srt_context* ctx);  /* also zeroes the NaN counter */
 /* Failure detection: path samples with a NaN component accumulated since the
  * context was created or srt_reset_stats (always counted, by the ordered
@@ -168,7 +175,7 @@ int srt_group_destroy(srt_group* g);
  * transport); "gathers.output" / "gathers.accum" (gathers issued so far); "bytes.output" /
  * "bytes.accum" (bytes one such gather moves into context 0, in KiB). */
 int srt_group_get_int(srt_group* g, const char* name, int* v);
-/* Each context's srt_last_kernel_ms (HIP events around its sample_kernel launches), n entries. */
+/* Each context's srt_last_kernel_ms (its sample launches' spans), n entries. */
 int srt_group_last_kernel_ms(srt_group* g, float* ms, int n);
 /* Uniform setters broadcast to every context (the names of srt_set_*). */
 int srt_group_set_bool(srt_group* g, const char* name, int v);

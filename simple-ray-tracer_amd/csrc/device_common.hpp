@@ -68,6 +68,7 @@ struct KParams {
   const uint32_t* tile_order;  // the launch's tiles in schedule order (nullptr: natural order)
   uint32_t* tile_cost;         // per tile: first-frame bounces recorded for the next launch's order (or nullptr)
   unsigned long long* wave_trace;  // diagnostic build (SRT_WAVE_TRACE): 4 stamps per wave
+  unsigned long long* span;        // {first wave's start, last wave's end} (s_memrealtime, 100 MHz), or nullptr
   const int* row_map;      // nranks > 1: the global row of each local row (row bands, pathtrace.hip FillParams)
 };
 

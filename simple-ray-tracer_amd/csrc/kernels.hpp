@@ -251,6 +251,9 @@ __device__ __forceinline__ int shade_hit(const KParams& kp, const Lane& ln, Coun
 template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX, bool FUSE, int GW, bool SPH>
 __device__ __forceinline__ void sample_body(const KParams& kp) {
   const int tid = threadIdx.x;
+  // the launch's span for its kernel time: pipelined launches overlap their neighbours, so HIP events
+  // around them would time the wait for CUs too (pathtrace.hip Launch); vector atomics on two words
+  if (kp.span && tid == 0) atomicMin(&kp.span[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #ifdef SRT_WAVE_TRACE
   const unsigned long long tw0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long tw2 = 0;
@@ -574,6 +577,7 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
   }
 #endif
   flush_counters<COUNT>(kp, c);
+  if (kp.span && lane == 0) atomicMax(&kp.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // A mesh scene (showModel set); FUSE/GW: global-scene mode's schedule and waves per SIMD.
@@ -619,6 +623,14 @@ __global__ __launch_bounds__(1024) void order_tiles_kernel(uint32_t* cost, uint3
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     order[atomicAdd(&hist[cost_bucket(cost[i])], 1u)] = (uint32_t)i;
     cost[i] = 0u;
+  }
+}
+
+// A launch's span record before the launch: {no start yet, no end yet}.
+__global__ void span_init_kernel(unsigned long long* span) {
+  if (threadIdx.x == 0) {
+    span[0] = ~0ull;
+    span[1] = 0ull;
   }
 }
 

@@ -189,12 +189,98 @@ struct srt_context {
   int trace_waves = 0;
 #endif
   int ev_used = 0;
+  // Pipelined sample launches (SRT_PIPELINE slots, default 3; 1: every launch on `stream`).  A timed
+  // sample_kernel / sphere_kernel launch goes on the next slot's own stream with the slot's sample
+  // buffer, batch counter, tile order and stacks; its accumulate_kernel stays on `stream` behind it.  A
+  // slot's next launch waits only for that slot's last accumulation, so launch k+1 fills the CUs that
+  // launch k's last waves leave idle (the drain) and the accumulations run beside them, instead of
+  // sample and accumulate alternating on one stream.  The tile order of a slot's launch comes from the
+  // costs of that slot's previous launch (the order decides which wave traces which sample, never a
+  // value).  Counting, pool and wavefront launches run on `stream` with the context's own buffers.
+  struct Slot {
+    hipStream_t stream = nullptr;
+    hipEvent_t sampled = nullptr, accumulated = nullptr;
+    bool pending = false;  // `accumulated` recorded since the slot's buffers were last known idle
+    float4* lbuf = nullptr;
+    size_t lbuf_bytes = 0;
+    unsigned long long* batch_ctr = nullptr;
+    int batch_ctr_cap = 0;
+    uint32_t* tile_cost = nullptr;
+    uint32_t* tile_order = nullptr;
+    int tile_cap = 0, tile_costs_for = -1;
+    uint32_t* gstack = nullptr;
+    size_t gstack_bytes = 0;
+  };
+  std::vector<Slot> slots;
+  int pipe = 3;                    // SRT_PIPELINE
+  // SRT_PIPELINE_OVERLAP: whether a sample launch may start before the previous one ends (2: always; 1, the
+  // default: on a rank's share of a multi-GPU split (nranks > 1), whose short launches lose ~3% to the
+  // drain; 0: never).  An overlapped launch's dispatch-to-end time (rocprofv3) and span include its wait
+  // for the CUs its predecessor still holds, so the 1-GPU launch the roofline is quoted on runs serially.
+  int pipe_overlap = 1;
+  hipEvent_t last_sampled = nullptr;  // the last sample launch's end (a slot's `sampled`, or plain_done)
+  hipEvent_t plain_done = nullptr;    // recorded on `stream` after a launch outside the slots
+  unsigned long long pipe_seq = 0;
+  hipStream_t lstream = nullptr;   // the stream the current launch's sample kernel goes on
+  // Kernel time of sample_kernel / sphere_kernel launches: each writes its span (first wave's start,
+  // last wave's end; s_memrealtime) into a record of this ring (HIP events around a pipelined launch
+  // would also time its wait for the CUs its predecessor still holds).
+  unsigned long long* d_span = nullptr;
+  static constexpr int kSpanCap = 1024;
+  unsigned long long span_seq = 0, span_read = 0;  // records written / summed by srt_kernel_time
+  std::vector<long long> chunk_span;               // per chunk of the last render: its record (or -1)
+  hipEvent_t lidle = nullptr;      // synchronized before the current launch frees a launch buffer
 };
 
 namespace {
 
 void FreeDev(void* p) {
   if (p) (void)hipFree(p);
+}
+
+int HipFail(const char* what) {
+  const hipError_t e = hipGetLastError();
+  srt::SetError(std::string(what) + ": " + hipGetErrorString(e));
+  return SRT_ERR_HIP;
+}
+
+// Waits until no pipelined sample launch is in flight: before anything rewrites or frees device data
+// those launches read (scene, lights, BVH records, noise, row map).
+int Quiesce(srt_context* c) {
+  for (auto& s : c->slots)
+    if (s.stream) HIP_OK(hipStreamSynchronize(s.stream));
+  return SRT_OK;
+}
+
+// The span record of the launch being set up (kernels.hpp sample_body), initialised on its stream.
+int TakeSpan(srt_context* c, srt::KParams& kp) {
+  if (!c->d_span) HIP_OK(hipMalloc(&c->d_span, sizeof(unsigned long long) * 2 * srt_context::kSpanCap));
+  const unsigned long long seq = c->span_seq++;
+  kp.span = c->d_span + 2 * (seq % srt_context::kSpanCap);
+  const size_t chunk = (size_t)(c->ev_used / 2);
+  if (c->chunk_span.size() <= chunk) c->chunk_span.resize(chunk + 1, -1);
+  c->chunk_span[chunk] = (long long)seq;
+  hipLaunchKernelGGL(srt::span_init_kernel, dim3(1), dim3(64), 0, c->lstream, kp.span);
+  HIP_OK(hipGetLastError());
+  return SRT_OK;
+}
+
+// The launch buffers of the context and of pipeline slot `s` trade places (in, launch, out again).
+// Launches in series share the context's tile costs and order (each orders its tiles by the costs of
+// the launch just before it, which has ended); overlapping launches each keep their slot's.
+void SwapSlot(srt_context* c, srt_context::Slot& s, bool tiles) {
+  std::swap(c->d_lbuf, s.lbuf);
+  std::swap(c->lbuf_bytes, s.lbuf_bytes);
+  std::swap(c->d_batch_ctr, s.batch_ctr);
+  std::swap(c->batch_ctr_cap, s.batch_ctr_cap);
+  if (tiles) {
+    std::swap(c->d_tile_cost, s.tile_cost);
+    std::swap(c->d_tile_order, s.tile_order);
+    std::swap(c->tile_cap, s.tile_cap);
+    std::swap(c->tile_costs_for, s.tile_costs_for);
+  }
+  std::swap(c->d_gstack, s.gstack);
+  std::swap(c->gstack_bytes, s.gstack_bytes);
 }
 
 int LocalRows(const srt_context* c, int H) {
@@ -229,6 +315,7 @@ int EnsureBvhs(srt_context* c) {
           return SRT_ERR_INVALID;
         }
   }
+  if (int rq = Quiesce(c)) return rq;
   if (need > c->bvh_capacity) {
     FreeDev(c->d_bvhs);
     c->d_bvhs = nullptr;
@@ -253,6 +340,7 @@ int EnsureLights(srt_context* c) {
     rec[2 * i] = make_float4(l.position[0], l.position[1], l.position[2], l.intensity);
     rec[2 * i + 1] = make_float4(l.color[0], l.color[1], l.color[2], 0.0f);
   }
+  if (int rq = Quiesce(c)) return rq;
   if (n > c->light_capacity) {
     FreeDev(c->d_lights);
     c->d_lights = nullptr;
@@ -351,6 +439,7 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
         const int band = ly / c->band_rows;
         rows[ly] = (band * c->nranks + c->rank) * c->band_rows + (ly - band * c->band_rows);
       }
+      if (int rq = Quiesce(c)) return rq;
       FreeDev(c->d_row_map);
       c->d_row_map = nullptr;
       c->row_map_key = -1;
@@ -395,6 +484,7 @@ int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
     const size_t lanes = (size_t)blocks * BLOCK;
     const size_t need = lanes * (PACK ? 2 : 3) * sizeof(uint32_t) * (size_t)kp.stack_entries;
     if (need > c->gstack_bytes) {
+      if (c->lidle) HIP_OK(hipEventSynchronize(c->lidle));
       FreeDev(c->d_gstack);
       c->d_gstack = nullptr;
       c->gstack_bytes = 0;
@@ -431,11 +521,12 @@ int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
   // 8 762-767, 10 793; profiles/r03_experiments/c5_pattern_threshold.txt)
   if constexpr (!LDSM && !FUSE && !COUNT)
     if (!c->trav_frac16_global_env) kp.trav_frac16 = 8;
-  HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
-  hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX, FUSE, GW>), dim3(blocks), dim3(BLOCK), lds, c->stream,
+  if (int rs = TakeSpan(c, kp)) return rs;
+  HIP_OK(hipEventRecord(c->ev[c->ev_used], c->lstream));
+  hipLaunchKernelGGL((srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX, FUSE, GW>), dim3(blocks), dim3(BLOCK), lds, c->lstream,
                      kp);
   HIP_OK(hipGetLastError());
-  HIP_OK(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
+  HIP_OK(hipEventRecord(c->ev[c->ev_used + 1], c->lstream));
   return SRT_OK;
 }
 
@@ -460,10 +551,11 @@ int LaunchSpheres(srt_context* c, srt::KParams kp, size_t lds) {
     const long long n_batches = (long long)((kp.W + 7) >> 3) * ((kp.local_rows + 7) >> 3) * kp.nframes;
     kp.tail_start = (int)std::max<long long>(0, n_batches - (long long)c->tail_claims_sph * srt::kClaimSph * waves);
   }
-  HIP_OK(hipEventRecord(c->ev[c->ev_used], c->stream));
-  hipLaunchKernelGGL(srt::sphere_kernel<COUNT>, dim3(blocks), dim3(256), lds, c->stream, kp);
+  if (int rs = TakeSpan(c, kp)) return rs;
+  HIP_OK(hipEventRecord(c->ev[c->ev_used], c->lstream));
+  hipLaunchKernelGGL(srt::sphere_kernel<COUNT>, dim3(blocks), dim3(256), lds, c->lstream, kp);
   HIP_OK(hipGetLastError());
-  HIP_OK(hipEventRecord(c->ev[c->ev_used + 1], c->stream));
+  HIP_OK(hipEventRecord(c->ev[c->ev_used + 1], c->lstream));
   return SRT_OK;
 }
 
@@ -807,14 +899,15 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   const int chunk = (int)std::max<size_t>(
       1, std::min<size_t>(std::min<size_t>((size_t)kp.nframes, max_frames), c->lbuf_cap / per_frame));
   const size_t need = per_frame * (size_t)chunk;
-  if (need > c->lbuf_bytes) {
-    FreeDev(c->d_lbuf);
-    c->d_lbuf = nullptr;
-    c->lbuf_bytes = 0;
-    HIP_OK(hipMalloc(&c->d_lbuf, need));
-    c->lbuf_bytes = need;
+  const bool piped = !count && !pool && !wf && c->pipe > 1;
+  if (piped && c->slots.empty()) {
+    c->slots.resize((size_t)c->pipe);
+    for (auto& sl : c->slots) {
+      HIP_OK(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+      HIP_OK(hipEventCreateWithFlags(&sl.sampled, hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&sl.accumulated, hipEventDisableTiming));
+    }
   }
-  kp.lbuf = c->d_lbuf;
   kp.trav_frac16 = ldsm ? c->trav_frac16 : c->trav_frac16_global;
   kp.bounce_cap = c->bounce_cap;
   // (ST_POOLERR, the last entry, is sticky: a watchdog that fired in an earlier launch of this
@@ -823,62 +916,138 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   HIP_OK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_POOLERR, c->stream));
   const int out_frames = kp.frame_first + kp.nframes - 1;
   const int nchunks = (kp.nframes + chunk - 1) / chunk;
-  if (nchunks > c->batch_ctr_cap) {
-    FreeDev(c->d_batch_ctr);
-    c->d_batch_ctr = nullptr;
-    c->batch_ctr_cap = 0;
-    HIP_OK(hipMalloc(&c->d_batch_ctr, sizeof(unsigned long long) * (size_t)nchunks));
-    c->batch_ctr_cap = nchunks;
-  }
-  HIP_OK(hipMemsetAsync(c->d_batch_ctr, 0, sizeof(unsigned long long) * (size_t)nchunks, c->stream));
   while ((int)c->ev.size() < 2 * nchunks) {
     hipEvent_t e;
     HIP_OK(hipEventCreate(&e));
     c->ev.push_back(e);
   }
   c->ev_used = 0;
-  for (int f0 = 0; f0 < kp.nframes; f0 += chunk) {
-    srt::KParams kc = kp;
-    kc.frame_first = kp.frame_first + f0;
-    kc.nframes = std::min(chunk, kp.nframes - f0);
-    kc.write_output = (f0 + chunk >= kp.nframes) ? kp.write_output : 0;
-    kc.batch_ctr = reinterpret_cast<uint32_t*>(c->d_batch_ctr + f0 / chunk);
-    {  // tile order: the tiles the last launch found most expensive first (SRT_TILE_ORDER=0: natural order)
-      const int nt = (int)n_tiles;
-      if (nt > c->tile_cap) {
-        FreeDev(c->d_tile_cost);
-        FreeDev(c->d_tile_order);
-        c->d_tile_cost = c->d_tile_order = nullptr;
-        c->tile_cap = 0;
-        HIP_OK(hipMalloc(&c->d_tile_cost, sizeof(uint32_t) * (size_t)nt));
-        HIP_OK(hipMalloc(&c->d_tile_order, sizeof(uint32_t) * (size_t)nt));
-        c->tile_cap = nt;
-        c->tile_costs_for = -1;
-      }
-      if (c->tile_schedule && c->tile_costs_for == nt) {
-        hipLaunchKernelGGL(srt::order_tiles_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_tile_cost, c->d_tile_order,
-                           nt);
-      } else {
-        hipLaunchKernelGGL(srt::iota_kernel, dim3((nt + 255) / 256), dim3(256), 0, c->stream, c->d_tile_order, nt);
-        if (c->tile_schedule) HIP_OK(hipMemsetAsync(c->d_tile_cost, 0, sizeof(uint32_t) * (size_t)nt, c->stream));
-      }
-      HIP_OK(hipGetLastError());
-      kc.tile_order = c->d_tile_order;
-      kc.tile_cost = c->tile_schedule ? c->d_tile_cost : nullptr;
-      c->tile_costs_for = c->tile_schedule ? nt : -1;
+  c->chunk_span.assign((size_t)nchunks, -1);
+  // The launch buffers: the context's own on `stream`, or (piped) one slot's per chunk on the slot's
+  // stream.  A piped chunk's batch counter is the slot's one word (its previous launch is accumulated).
+  const int ctr_need = piped ? 1 : nchunks;
+  const bool overlap = c->pipe_overlap == 2 || (c->pipe_overlap == 1 && c->nranks > 1);
+  if (piped) {  // every slot's sample buffer now, so a timed loop after one warmup render allocates none
+    for (auto& sl : c->slots) {
+      if (sl.lbuf_bytes >= need) continue;
+      if (sl.pending) HIP_OK(hipEventSynchronize(sl.accumulated));
+      FreeDev(sl.lbuf);
+      sl.lbuf = nullptr;
+      sl.lbuf_bytes = 0;
+      HIP_OK(hipMalloc(&sl.lbuf, need));
+      sl.lbuf_bytes = need;
     }
-    int rc;
-    // LDS mode: packed entries (lds_ok); global-scene mode: packed when indices fit 24 bits
-    const bool pack = c->lds_ok;
-    if (pool) rc = count ? LaunchPool<true>(c, kc, lds) : LaunchPool<false>(c, kc, lds);
-    else if (wf) rc = LaunchWavefront(c, kc, c->sample_textures);
-    else rc = c->sample_textures ? LaunchMode<true>(c, kc, lds, count, ldsm, pack)
-                                 : LaunchMode<false>(c, kc, lds, count, ldsm, pack);
+  }
+  for (int f0 = 0; f0 < kp.nframes; f0 += chunk) {
+    srt_context::Slot* sl = piped ? &c->slots[(size_t)(c->pipe_seq++ % (unsigned long long)c->pipe)] : nullptr;
+    if (sl) {
+      if (sl->pending) HIP_OK(hipStreamWaitEvent(sl->stream, sl->accumulated, 0));
+      if (!overlap && c->last_sampled) HIP_OK(hipStreamWaitEvent(sl->stream, c->last_sampled, 0));
+      SwapSlot(c, *sl, overlap);
+      c->lstream = sl->stream;
+      c->lidle = sl->pending ? sl->accumulated : nullptr;
+    }
+    const hipStream_t ls = c->lstream;
+    int rc = SRT_OK;
+    do {  // (one pass: `break` on an error, so the slot's buffers are swapped back)
+      const bool grow = need > c->lbuf_bytes || ctr_need > c->batch_ctr_cap || (int)n_tiles > c->tile_cap;
+      if (grow && c->lidle) {  // the slot's last launch still reads the buffers being replaced
+        if (hipEventSynchronize(c->lidle) != hipSuccess) { rc = HipFail("sample launch"); break; }
+      }
+      if (need > c->lbuf_bytes) {
+        FreeDev(c->d_lbuf);
+        c->d_lbuf = nullptr;
+        c->lbuf_bytes = 0;
+        if (hipMalloc(&c->d_lbuf, need) != hipSuccess) { srt::SetError("hipMalloc(sample buffer) failed"); rc = SRT_ERR_HIP; break; }
+        c->lbuf_bytes = need;
+      }
+      if (ctr_need > c->batch_ctr_cap) {
+        FreeDev(c->d_batch_ctr);
+        c->d_batch_ctr = nullptr;
+        c->batch_ctr_cap = 0;
+        if (hipMalloc(&c->d_batch_ctr, sizeof(unsigned long long) * (size_t)ctr_need) != hipSuccess) {
+          srt::SetError("hipMalloc(batch counters) failed");
+          rc = SRT_ERR_HIP;
+          break;
+        }
+        c->batch_ctr_cap = ctr_need;
+      }
+      if (!sl && f0 == 0)
+        if (hipMemsetAsync(c->d_batch_ctr, 0, sizeof(unsigned long long) * (size_t)nchunks, ls) != hipSuccess) { rc = HipFail("sample launch"); break; }
+      if (sl && hipMemsetAsync(c->d_batch_ctr, 0, sizeof(unsigned long long), ls) != hipSuccess) { rc = HipFail("sample launch"); break; }
+      srt::KParams kc = kp;
+      kc.lbuf = c->d_lbuf;
+      kc.frame_first = kp.frame_first + f0;
+      kc.nframes = std::min(chunk, kp.nframes - f0);
+      kc.write_output = (f0 + chunk >= kp.nframes) ? kp.write_output : 0;
+      kc.batch_ctr = reinterpret_cast<uint32_t*>(c->d_batch_ctr + (sl ? 0 : f0 / chunk));
+      {  // tile order: the tiles the last launch found most expensive first (SRT_TILE_ORDER=0: natural order)
+        const int nt = (int)n_tiles;
+        if (nt > c->tile_cap) {
+          FreeDev(c->d_tile_cost);
+          FreeDev(c->d_tile_order);
+          c->d_tile_cost = c->d_tile_order = nullptr;
+          c->tile_cap = 0;
+          if (hipMalloc(&c->d_tile_cost, sizeof(uint32_t) * (size_t)nt) != hipSuccess ||
+              hipMalloc(&c->d_tile_order, sizeof(uint32_t) * (size_t)nt) != hipSuccess) {
+            srt::SetError("hipMalloc(tile order) failed");
+            rc = SRT_ERR_HIP;
+            break;
+          }
+          c->tile_cap = nt;
+          c->tile_costs_for = -1;
+        }
+        if (c->tile_schedule && c->tile_costs_for == nt) {
+          hipLaunchKernelGGL(srt::order_tiles_kernel, dim3(1), dim3(1024), 0, ls, c->d_tile_cost, c->d_tile_order, nt);
+        } else {
+          hipLaunchKernelGGL(srt::iota_kernel, dim3((nt + 255) / 256), dim3(256), 0, ls, c->d_tile_order, nt);
+          if (c->tile_schedule && hipMemsetAsync(c->d_tile_cost, 0, sizeof(uint32_t) * (size_t)nt, ls) != hipSuccess) {
+            rc = HipFail("sample launch");
+            break;
+          }
+        }
+        if (hipGetLastError() != hipSuccess) { rc = HipFail("sample launch"); break; }
+        kc.tile_order = c->d_tile_order;
+        kc.tile_cost = c->tile_schedule ? c->d_tile_cost : nullptr;
+        c->tile_costs_for = c->tile_schedule ? nt : -1;
+      }
+      // LDS mode: packed entries (lds_ok); global-scene mode: packed when indices fit 24 bits
+      const bool pack = c->lds_ok;
+      if (pool) rc = count ? LaunchPool<true>(c, kc, lds) : LaunchPool<false>(c, kc, lds);
+      else if (wf) rc = LaunchWavefront(c, kc, c->sample_textures);
+      else rc = c->sample_textures ? LaunchMode<true>(c, kc, lds, count, ldsm, pack)
+                                   : LaunchMode<false>(c, kc, lds, count, ldsm, pack);
+      if (rc) break;
+      c->pool_launched |= pool;
+      c->ev_used += 2;  // LaunchSamples recorded the pair around the launch
+      if (!sl) {  // a later launch in series (sharing the tile order) waits for this one
+        if (!c->plain_done && hipEventCreateWithFlags(&c->plain_done, hipEventDisableTiming) != hipSuccess) {
+          rc = HipFail("sample launch");
+          break;
+        }
+        if (hipEventRecord(c->plain_done, c->stream) != hipSuccess) { rc = HipFail("sample launch"); break; }
+        c->last_sampled = c->plain_done;
+      }
+      if (sl) {  // the accumulation follows the samples on `stream`
+        c->last_sampled = sl->sampled;
+        if (hipEventRecord(sl->sampled, ls) != hipSuccess || hipStreamWaitEvent(c->stream, sl->sampled, 0) != hipSuccess) {
+          rc = HipFail("sample launch");
+          break;
+        }
+      }
+      hipLaunchKernelGGL(srt::accumulate_kernel, pgrid, dim3(256), 0, c->stream, kc, out_frames);
+      if (hipGetLastError() != hipSuccess) { rc = HipFail("sample launch"); break; }
+      if (sl) {
+        if (hipEventRecord(sl->accumulated, c->stream) != hipSuccess) { rc = HipFail("sample launch"); break; }
+        sl->pending = true;
+      }
+    } while (false);
+    if (sl) {
+      SwapSlot(c, *sl, overlap);
+      c->lstream = c->stream;
+      c->lidle = nullptr;
+    }
     if (rc) return rc;
-    c->pool_launched |= pool;
-    c->ev_used += 2;  // LaunchSamples recorded the pair around the launch
-    hipLaunchKernelGGL(srt::accumulate_kernel, pgrid, dim3(256), 0, c->stream, kc, out_frames);
-    HIP_OK(hipGetLastError());
   }
   if (count) {
     unsigned long long s[srt::ST_N];
@@ -1114,6 +1283,8 @@ int srt_create(int device, void* stream, srt_context** out) {
   if (const char* e = std::getenv("SRT_WF_WAVES")) c->wf_waves = std::atoi(e);
   if (const char* e = std::getenv("SRT_TREELETS")) c->treelets = e[0] == '1' ? 1 : 0;
   if (const char* e = std::getenv("SRT_TREELET_DEPTH")) c->treelet_depth = std::max(0, std::min(srt::kTopStack - 1, std::atoi(e)));
+  if (const char* e = std::getenv("SRT_PIPELINE")) c->pipe = std::max(1, std::min(8, std::atoi(e)));
+  if (const char* e = std::getenv("SRT_PIPELINE_OVERLAP")) c->pipe_overlap = std::max(0, std::min(2, std::atoi(e)));
   if (const char* e = std::getenv("SRT_TAIL_CLAIMS")) c->tail_claims = c->tail_claims_sph = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("SRT_TILE_ORDER")) c->tile_schedule = e[0] != '0';
   if (const char* e = std::getenv("SRT_TRAV_FRAC16")) c->trav_frac16 = std::max(0, std::min(16, std::atoi(e)));
@@ -1135,6 +1306,7 @@ int srt_create(int device, void* stream, srt_context** out) {
     }
     c->own_stream = true;
   }
+  c->lstream = c->stream;
   if (hipMalloc(&c->d_stats, sizeof(unsigned long long) * srt::ST_TOTAL) != hipSuccess ||
       hipMemset(c->d_stats, 0, sizeof(unsigned long long) * srt::ST_TOTAL) != hipSuccess ||
       hipMalloc(&c->d_nan, sizeof(unsigned long long)) != hipSuccess ||
@@ -1154,10 +1326,19 @@ int srt_destroy(srt_context* c) {
   if (!c) return SRT_ERR_INVALID;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)Quiesce(c);
+  for (auto& sl : c->slots) {
+    FreeDev(sl.lbuf); FreeDev(sl.batch_ctr); FreeDev(sl.tile_cost); FreeDev(sl.tile_order); FreeDev(sl.gstack);
+    if (sl.sampled) (void)hipEventDestroy(sl.sampled);
+    if (sl.accumulated) (void)hipEventDestroy(sl.accumulated);
+    if (sl.stream) (void)hipStreamDestroy(sl.stream);
+  }
+  c->slots.clear();
+  if (c->plain_done) (void)hipEventDestroy(c->plain_done);
   FreeDev(c->d_nodes); FreeDev(c->d_tris); FreeDev(c->d_mats); FreeDev(c->d_bvhs); FreeDev(c->d_lights);
   FreeDev(c->d_tex); FreeDev(c->d_tex_info); FreeDev(c->d_tri_uv);
   FreeDev(c->d_noise_xy); FreeDev(c->d_noise_u); FreeDev(c->d_stats); FreeDev(c->d_nan); FreeDev(c->d_lbuf); FreeDev(c->d_gstack);
-  FreeDev(c->d_batch_ctr); FreeDev(c->d_tile_cost); FreeDev(c->d_tile_order); FreeDev(c->d_row_map);
+  FreeDev(c->d_batch_ctr); FreeDev(c->d_tile_cost); FreeDev(c->d_tile_order); FreeDev(c->d_row_map); FreeDev(c->d_span);
   FreeDev(c->d_wf_rec); FreeDev(c->d_wf_res); FreeDev(c->d_wf_state); FreeDev(c->d_wf_rayq); FreeDev(c->d_wf_hitq);
   FreeDev(c->d_wf_ctl); FreeDev(c->d_wf_items);
   FreeDev(c->d_nodes_t); FreeDev(c->d_troot); FreeDev(c->d_tl_ray); FreeDev(c->d_tl_stk); FreeDev(c->d_tl_slist);
@@ -1340,10 +1521,40 @@ int srt_last_kernel_ms(srt_context* c, float* ms) {
   *ms = 0.0f;
   for (int i = 0; i + 1 < c->ev_used; i += 2) {
     HIP_OK(hipEventSynchronize(c->ev[i + 1]));
-    float t = 0.0f;
+    const size_t chunk = (size_t)(i / 2);
+    const long long rec = chunk < c->chunk_span.size() ? c->chunk_span[chunk] : -1;
+    if (rec >= 0 && (unsigned long long)rec + srt_context::kSpanCap >= c->span_seq) {  // the launch's own span
+      unsigned long long sp[2];
+      HIP_OK(hipMemcpy(sp, c->d_span + 2 * ((unsigned long long)rec % srt_context::kSpanCap), sizeof sp,
+                       hipMemcpyDeviceToHost));
+      if (sp[1] >= sp[0]) *ms += (float)((double)(sp[1] - sp[0]) * 1e-5);  // 100 MHz ticks
+      continue;
+    }
+    float t = 0.0f;  // pool and wavefront launches: the HIP events around them
     HIP_OK(hipEventElapsedTime(&t, c->ev[i], c->ev[i + 1]));
     *ms += t;
   }
+  return SRT_OK;
+}
+
+int srt_kernel_time(srt_context* c, double* total_ms, int* launches) {
+  if (!c || !total_ms || !launches) return SRT_ERR_INVALID;
+  *total_ms = 0.0;
+  *launches = 0;
+  HIP_OK(hipStreamSynchronize(c->stream));
+  if (int rq = Quiesce(c)) return rq;
+  unsigned long long from = c->span_read;
+  if (c->span_seq - from > (unsigned long long)srt_context::kSpanCap) from = c->span_seq - srt_context::kSpanCap;
+  if (c->span_seq > from) {
+    std::vector<unsigned long long> all(2 * srt_context::kSpanCap);
+    HIP_OK(hipMemcpy(all.data(), c->d_span, sizeof(unsigned long long) * all.size(), hipMemcpyDeviceToHost));
+    for (unsigned long long q = from; q < c->span_seq; ++q) {
+      const unsigned long long* sp = &all[2 * (q % srt_context::kSpanCap)];
+      if (sp[1] >= sp[0]) *total_ms += (double)(sp[1] - sp[0]) * 1e-5;
+      ++*launches;
+    }
+  }
+  c->span_read = c->span_seq;
   return SRT_OK;
 }
 
@@ -1378,6 +1589,7 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   if (!c || (n_bvhs && !bvhs) || (n_nodes && !nodes) || (n_mats && !mats) || (n_tris && !tris) ||
       (n_verts && !verts))
     return SRT_ERR_INVALID;
+  if (int rq = Quiesce(c)) return rq;  // pipelined launches still read the old scene
   if (n_nodes == 0 || n_bvhs == 0) {
     srt::SetError("scene needs at least one BVH and one node");
     return SRT_ERR_INVALID;
@@ -1626,6 +1838,7 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
 
 int srt_upload_textures(srt_context* c, const srt_texture* textures, uint32_t n) {
   if (!c || (n && !textures)) return SRT_ERR_INVALID;
+  if (int rq = Quiesce(c)) return rq;
   std::vector<uint4> info(std::max<uint32_t>(n, 1), make_uint4(0, 0, 0, 0));
   size_t total = 0;
   for (uint32_t i = 0; i < n; ++i) {
@@ -1687,6 +1900,7 @@ int srt_set_lights(srt_context* c, const srt_light* lights, uint32_t n) {
 int srt_set_noise(srt_context* c, const float* noise_rgb, const float* noise_u_rgb, size_t texels) {
   if (!c || !noise_rgb || !noise_u_rgb || texels == 0) return SRT_ERR_INVALID;
   HIP_OK(hipSetDevice(c->device));
+  if (int rq = Quiesce(c)) return rq;
   std::vector<float2> xy(texels);
   std::vector<float> u(texels);
   for (size_t i = 0; i < texels; ++i) {

@@ -520,10 +520,16 @@ class Compute:
         return s.as_dict()
 
     def last_kernel_ms(self) -> float:
-        """Device time of the sample-kernel launches of the last render (HIP events on the launch stream)."""
+        """Device time of the sample-kernel launches of the last render (each launch's span on the GPU clock)."""
         ms = C.c_float()
         check(lib().srt_last_kernel_ms(self.ctx, C.byref(ms)), "last_kernel_ms")
         return float(ms.value)
+
+    def kernel_time(self) -> tuple:
+        """(summed kernel ms, launches) of the sample-kernel launches since the previous call."""
+        ms, n = C.c_double(), C.c_int()
+        check(lib().srt_kernel_time(self.ctx, C.byref(ms), C.byref(n)), "kernel_time")
+        return float(ms.value), int(n.value)
 
     def reset_stats(self):
         check(lib().srt_reset_stats(self.ctx), "reset_stats")

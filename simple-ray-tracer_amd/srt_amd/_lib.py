@@ -102,6 +102,7 @@ _SIGS = {
     "srt_render_frames": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int]),
     "srt_get_stats": (C.c_int, [P, C.POINTER(Stats)]),
     "srt_last_kernel_ms": (C.c_int, [P, C.POINTER(C.c_float)]),
+    "srt_kernel_time": (C.c_int, [P, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     "srt_reset_stats": (C.c_int, [P]),
     "srt_nan_samples": (C.c_int, [P, C.POINTER(C.c_uint64)]),
     "srt_checkpoint_save": (C.c_int, [P, C.c_char_p]),

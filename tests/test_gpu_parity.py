@@ -666,3 +666,36 @@ def test_pool_kernel_metric_frame_equals_sample_kernel(rubik, monkeypatch):
     monkeypatch.setenv("SRT_POOL", "1")
     b, p, st2 = gpu_render(setup, 16)
     assert bits_equal(a, b).all() and (o == p).all() and st["rays"] == st2["rays"]
+
+
+@pytest.mark.parametrize("scene", ["rubik", "spheres", "global"])
+def test_pipelined_launches_match_one_stream(rubik, monkeypatch, scene):
+    """Pipelined sample launches (SRT_PIPELINE slots, each its own stream and launch buffers; launches
+    overlapping each other or in series, SRT_PIPELINE_OVERLAP): renders enqueued back to back, in many small chunks (a small sample buffer) so that every slot is reused with
+    its tile order from its previous launch, give the frame of the one-stream build bit for bit; and
+    srt_kernel_time counts every launch."""
+    if scene == "global":
+        monkeypatch.setenv("SRT_FORCE_GLOBAL_SCENE", "1")
+    setup = (R.make_setup(56, 40, show_model=False, max_depth=4) if scene == "spheres"
+             else R.make_setup(56, 40, show_model=True, models=[rubik]))
+    monkeypatch.setenv("SRT_SAMPLE_BUFFER_KB", str(56 * 40 * 16 * 3 // 1024 + 1))  # 3 frames per chunk
+    got = {}
+    for pipe, overlap in (("1", "1"), ("3", "2"), ("2", "2"), ("3", "1")):  # 1: overlap only for nranks > 1
+        monkeypatch.setenv("SRT_PIPELINE", pipe)
+        monkeypatch.setenv("SRT_PIPELINE_OVERLAP", overlap)
+        r = R.Renderer(setup)
+        try:
+            r.compute.kernel_time()
+            for _ in range(3):  # no finish between the renders
+                r.render(16, write_output=True)
+            r.finish()
+            ms, launches = r.compute.kernel_time()
+            assert launches == 3 * 6 and ms > 0.0  # 16 frames in chunks of 3: 6 launches per render
+            got[pipe + "/" + overlap] = (r.accum(), r.output())
+        finally:
+            r.close()
+    for key in ("3/2", "2/2", "3/1"):
+        assert bits_equal(got[key][0], got["1/1"][0]).all(), f"SRT_PIPELINE/OVERLAP={key}"
+        assert (got[key][1] == got["1/1"][1]).all()
+    acc, out, _ = oracle_render(setup, 16)
+    assert bits_equal(got["3/2"][0], acc).all() and (got["3/2"][1] == out).all()
