@@ -135,6 +135,20 @@ class Compute {
   }
   // glMemoryBarrier + glFinish (src/main.cpp:709-718)
   void Finish() { check(srt_finish(context()), "Finish"); }
+  // Device time of the last render's sample launches, and the summed time of every sample launch since
+  // the previous KernelTime call (each launch's span on the GPU clock; srt_amd.h)
+  float LastKernelMs() {
+    float ms = 0.0f;
+    check(srt_last_kernel_ms(context(), &ms), "LastKernelMs");
+    return ms;
+  }
+  double KernelTime(int* launches = nullptr) {
+    double ms = 0.0;
+    int n = 0;
+    check(srt_kernel_time(context(), &ms, &n), "KernelTime");
+    if (launches) *launches = n;
+    return ms;
+  }
 
   // `n` progressive frames in one launch (same accumulation as n Dispatch calls)
   void RenderFrames(int frame_first, int n, bool write_output = true) {

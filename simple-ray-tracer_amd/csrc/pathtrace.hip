@@ -230,6 +230,7 @@ struct srt_context {
   unsigned long long span_seq = 0, span_read = 0;  // records written / summed by srt_kernel_time
   std::vector<long long> chunk_span;               // per chunk of the last render: its record (or -1)
   hipEvent_t lidle = nullptr;      // synchronized before the current launch frees a launch buffer
+  hipEvent_t lidle2 = nullptr;     // (and this: the previous launch, for the buffers launches in series share)
 };
 
 namespace {
@@ -252,6 +253,13 @@ int Quiesce(srt_context* c) {
   return SRT_OK;
 }
 
+// Before the launch being set up frees one of its buffers: the launches that may still read it are done.
+int WaitLaunchIdle(srt_context* c) {
+  if (c->lidle) HIP_OK(hipEventSynchronize(c->lidle));
+  if (c->lidle2) HIP_OK(hipEventSynchronize(c->lidle2));
+  return SRT_OK;
+}
+
 // The span record of the launch being set up (kernels.hpp sample_body), initialised on its stream.
 int TakeSpan(srt_context* c, srt::KParams& kp) {
   if (!c->d_span) HIP_OK(hipMalloc(&c->d_span, sizeof(unsigned long long) * 2 * srt_context::kSpanCap));
@@ -267,20 +275,21 @@ int TakeSpan(srt_context* c, srt::KParams& kp) {
 
 // The launch buffers of the context and of pipeline slot `s` trade places (in, launch, out again).
 // Launches in series share the context's tile costs and order (each orders its tiles by the costs of
-// the launch just before it, which has ended); overlapping launches each keep their slot's.
-void SwapSlot(srt_context* c, srt_context::Slot& s, bool tiles) {
+// the launch just before it, which has ended) and its global stacks; overlapping launches each keep
+// their slot's.
+void SwapSlot(srt_context* c, srt_context::Slot& s, bool own) {
   std::swap(c->d_lbuf, s.lbuf);
   std::swap(c->lbuf_bytes, s.lbuf_bytes);
   std::swap(c->d_batch_ctr, s.batch_ctr);
   std::swap(c->batch_ctr_cap, s.batch_ctr_cap);
-  if (tiles) {
+  if (own) {
     std::swap(c->d_tile_cost, s.tile_cost);
     std::swap(c->d_tile_order, s.tile_order);
     std::swap(c->tile_cap, s.tile_cap);
     std::swap(c->tile_costs_for, s.tile_costs_for);
+    std::swap(c->d_gstack, s.gstack);
+    std::swap(c->gstack_bytes, s.gstack_bytes);
   }
-  std::swap(c->d_gstack, s.gstack);
-  std::swap(c->gstack_bytes, s.gstack_bytes);
 }
 
 int LocalRows(const srt_context* c, int H) {
@@ -484,7 +493,7 @@ int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
     const size_t lanes = (size_t)blocks * BLOCK;
     const size_t need = lanes * (PACK ? 2 : 3) * sizeof(uint32_t) * (size_t)kp.stack_entries;
     if (need > c->gstack_bytes) {
-      if (c->lidle) HIP_OK(hipEventSynchronize(c->lidle));
+      if (int rw = WaitLaunchIdle(c)) return rw;
       FreeDev(c->d_gstack);
       c->d_gstack = nullptr;
       c->gstack_bytes = 0;
@@ -946,14 +955,17 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
       SwapSlot(c, *sl, overlap);
       c->lstream = sl->stream;
       c->lidle = sl->pending ? sl->accumulated : nullptr;
+      c->lidle2 = overlap ? nullptr : c->last_sampled;
+    }
+    if (!sl) {  // launches in series may still read the shared stacks and tile arrays
+      c->lidle = nullptr;
+      c->lidle2 = c->last_sampled;
     }
     const hipStream_t ls = c->lstream;
     int rc = SRT_OK;
     do {  // (one pass: `break` on an error, so the slot's buffers are swapped back)
       const bool grow = need > c->lbuf_bytes || ctr_need > c->batch_ctr_cap || (int)n_tiles > c->tile_cap;
-      if (grow && c->lidle) {  // the slot's last launch still reads the buffers being replaced
-        if (hipEventSynchronize(c->lidle) != hipSuccess) { rc = HipFail("sample launch"); break; }
-      }
+      if (grow && WaitLaunchIdle(c) != SRT_OK) { rc = SRT_ERR_HIP; break; }  // earlier launches still read them
       if (need > c->lbuf_bytes) {
         FreeDev(c->d_lbuf);
         c->d_lbuf = nullptr;
@@ -1045,8 +1057,8 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
     if (sl) {
       SwapSlot(c, *sl, overlap);
       c->lstream = c->stream;
-      c->lidle = nullptr;
     }
+    c->lidle = c->lidle2 = nullptr;
     if (rc) return rc;
   }
   if (count) {
