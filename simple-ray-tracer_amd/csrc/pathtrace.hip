@@ -909,7 +909,8 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
       1, std::min<size_t>(std::min<size_t>((size_t)kp.nframes, max_frames), c->lbuf_cap / per_frame));
   const size_t need = per_frame * (size_t)chunk;
   const bool piped = !count && !pool && !wf && c->pipe > 1;
-  if (piped && c->slots.empty()) {
+  // (a counting launch, the untimed first launch of a measurement, sets the slots up for the timed ones)
+  if ((piped || (count && c->pipe > 1)) && c->slots.empty()) {
     c->slots.resize((size_t)c->pipe);
     for (auto& sl : c->slots) {
       HIP_OK(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
@@ -936,7 +937,7 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   // stream.  A piped chunk's batch counter is the slot's one word (its previous launch is accumulated).
   const int ctr_need = piped ? 1 : nchunks;
   const bool overlap = c->pipe_overlap == 2 || (c->pipe_overlap == 1 && c->nranks > 1);
-  if (piped) {  // every slot's sample buffer now, so a timed loop after one warmup render allocates none
+  if (piped || (count && c->pipe > 1)) {  // every slot's sample buffer now: a timed loop allocates none
     for (auto& sl : c->slots) {
       if (sl.lbuf_bytes >= need) continue;
       if (sl.pending) HIP_OK(hipEventSynchronize(sl.accumulated));
