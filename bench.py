@@ -157,7 +157,8 @@ def code_hash() -> str:
     return _lib.lib().srt_code_hash().decode()
 
 
-def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str, global_mode: bool = False) -> dict:
+def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str, global_mode: bool = False,
+             scale: float = 1.0) -> dict:
     """Roofs of the dominant kernel, fractions of the live kernel time (each launch's span on the GPU clock, srt_kernel_time):
     VALU issue (SQ_INSTS_VALU x 2 cycles per SIMD-32 over 1024 SIMDs), LDS-array cycles
     (SQ_LDS_IDX_ACTIVE over 256 CUs), HBM (corrected FETCH_SIZE + WRITE_SIZE over 8 TB/s).  The counters
@@ -183,6 +184,9 @@ def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str, globa
                   "note": "no committed PMC counters for this workload (profiles/counters.json): roofs unmeasured; "
                           "algorithmic_GBps = SURVEY 8d bytes per launch / kernel time"})
         return r
+    if scale != 1.0:  # a rank's share of the 1-GPU launch (its share of the counted rays)
+        cnt = {k: (v * scale if isinstance(v, (int, float)) else v) for k, v in cnt.items()}
+        r["counters_scaled_by_ray_share"] = round(scale, 5)
     valu_gips = cnt["SQ_INSTS_VALU"] / k_s / 1e9
     lds_gcps = cnt["SQ_LDS_IDX_ACTIVE"] / k_s / 1e9
     hbm_bytes = cnt["hbm_bytes"]
@@ -261,6 +265,7 @@ class RankRun:
         self.out_local = torch.zeros((self.rows_pad, W), dtype=torch.int32, device=self.dev)
         self.c.set_image_buffers(self.accum_local.data_ptr(), self.out_local.data_ptr())
         self.recv_out = self.full_out = None
+        self.ex_events = []
         if rank == 0 and world > 1:
             self.recv_out = torch.empty((world, self.rows_pad, W), dtype=torch.int32, device=self.dev)
             self.full_out = torch.zeros((H, W), dtype=torch.int32, device=self.dev)
@@ -274,27 +279,47 @@ class RankRun:
         return self.c.stats()
 
     def step(self):
+        import torch
+
         from srt_amd import parallel as PAR
 
         self.rdr.clear()
         self.c.render_frames(2, self.spp, write_output=True, count=False)
         self.rdr.accum_frames = self.spp + 1
         if self.world > 1:  # the one exchange: every rank's sRGB8 rows to rank 0 (RCCL over xGMI)
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()  # (the shared stream: after this rank's accumulation, i.e. its rows rendered)
             PAR.gather_bands(self.out_local, dst=0, out=self.recv_out)
             if self.rank == 0:
                 self.c.assemble_output_bands(self.recv_out.data_ptr(), self.world, self.rows_pad, self.band,
                                              self.full_out.data_ptr())
+            ev[1].record()
+            self.ex_events.append(ev)
+
+    def exchange_time(self) -> list:
+        """[(ms, frames)] of this rank's part of the per-frame exchange since the last call (events on the
+        shared stream around the gather and, on rank 0, the assembly)."""
+        import torch
+
+        torch.cuda.synchronize(self.dev)
+        ms = sum(a.elapsed_time(b) for a, b in self.ex_events)
+        n = len(self.ex_events)
+        self.ex_events = []
+        return [(ms, n)]
+
+    def chunks(self) -> list:
+        return [self.c.GetInt("launch.chunks")]  # sample launches of the last render
+
+    def overlaps(self) -> list:
+        return [self.c.GetInt("launch.overlap")]  # the last render's launches overlapped their predecessors
 
     def sync(self):
         import torch
 
         torch.cuda.synchronize(self.dev)
 
-    def kernel_ms(self) -> list:
-        return [self.c.last_kernel_ms()]  # the last render's sample launches (their spans on the GPU clock)
-
-    def kernel_time(self) -> tuple:
-        return self.c.kernel_time()  # (summed ms, launches) since the previous call
+    def kernel_time(self) -> list:
+        return [self.c.kernel_time()]  # [(throughput ms, launches)] since the previous call
 
     def frame(self):
         """Rank 0's frame after a step: (accum (H, W, 4) float32, sRGB8 (H, W, 4) uint8) on the host; None
@@ -337,6 +362,8 @@ class GroupRun:
         self.devices = list(devices)
         self.grp = R.GroupRenderer(setup, self.devices, band_rows=band_rows)
         self.enqueue_s = []
+        if self.grp.transport == "rccl" and self.grp.get_int("ranks") != len(self.devices):  # (the library checks too)
+            raise SystemExit(f"RCCL sees {self.grp.get_int('ranks')} ranks, not {len(self.devices)}")
 
     def count(self) -> dict:
         return self.grp.count(self.spp)
@@ -349,8 +376,20 @@ class GroupRun:
     def sync(self):
         self.grp.finish()
 
-    def kernel_ms(self) -> list:
-        return self.grp.kernel_ms()
+    def kernel_time(self) -> list:
+        return self.grp.kernel_time()  # per context: (throughput ms, launches) since the previous call
+
+    def exchange_time(self) -> list:
+        return self.grp.exchange_time()  # per context: (ms of its part of the exchange, frames)
+
+    def chunks(self) -> list:
+        return [p.compute.GetInt("launch.chunks") for p in self.grp.parts]
+
+    def overlaps(self) -> list:
+        return [p.compute.GetInt("launch.overlap") for p in self.grp.parts]
+
+    def rank_stats(self) -> list:
+        return self.grp.part_stats
 
     def frame(self):
         return self.grp.accum(), self.grp.output()
@@ -368,9 +407,10 @@ class GroupRun:
 
 
 def run_leg(setup, spp, args, *, mode, rank, world, device, stream):
-    """Counting run, warmup, then exactly `steps` timed steps bracketed by barrier + synchronize;
-    returns (elapsed max over ranks, total rays over ranks, this rank's stats, per-context kernel ms lists,
-    run)."""
+    """Counting run, warmup, then exactly `steps` timed steps enqueued back to back and bracketed by
+    barrier + synchronize; every context's kernel time (its launches' throughput time, srt_kernel_time)
+    and part of the per-frame exchange are read once, after the region.  Returns (elapsed max over ranks,
+    total rays over ranks, this process's stats, per-context timing dicts, run)."""
     import torch
     import torch.distributed as dist
 
@@ -391,47 +431,56 @@ def run_leg(setup, spp, args, *, mode, rank, world, device, stream):
     if mode == "dist" and world > 1:
         dist.barrier()
     run.sync()
-    # RankRun's steps are enqueued back to back (its sample launches are pipelined, DESIGN.md section 5:
-    # launch k+1 fills the CUs launch k's last waves leave idle); their kernel time is read once, after
-    # the timed region, from the launches' own spans.  The in-process group synchronises every step.
-    per_step_sync = mode == "group"
-    kernel_ms = []
-    if not per_step_sync:
-        run.kernel_time()  # drops the counting and warmup launches
+    run.kernel_time()    # drops the counting and warmup launches
+    run.exchange_time()  # (and the warmup's exchanges)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run.step()
-        if per_step_sync:
-            run.sync()
-            kernel_ms.append(run.kernel_ms())
     run.sync()
     if mode == "dist" and world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    if not per_step_sync:
-        total_ms, _launches = run.kernel_time()
-        kernel_ms = [[total_ms / args.steps]] * args.steps  # per step (one launch per step unless chunked)
+    kt, ex, chunks, ovl = run.kernel_time(), run.exchange_time(), run.chunks(), run.overlaps()
+    per_ctx = []
+    for i, ((ms, launches), (ex_ms, ex_n), ch, ov) in enumerate(zip(kt, ex, chunks, ovl)):
+        # every timed launch is counted (a chunked render makes several per step), or the total is short
+        if launches != args.steps * ch:
+            raise SystemExit(f"context {i}: {launches} sample launches timed, expected {args.steps} steps x {ch}")
+        per_ctx.append({"kernel_ms": ms / args.steps, "launches_per_step": ch, "overlap": bool(ov),
+                        "exchange_ms": (ex_ms / ex_n) if ex_n else None})
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64)
     if mode == "dist" and world > 1:
         elapsed = elapsed.to(run.dev) if args.backend == "nccl" else elapsed
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    per_ctx = [list(x) for x in zip(*kernel_ms)]  # [context][step]
     return float(elapsed.item()), total_rays, st, per_ctx, run
 
 
-def ranks_kernel_ms(per_ctx, args, mode, world, dev):
-    """Mean sample-kernel ms of every rank (context), rank order; under torch.distributed one all_gather."""
-    import torch
+def rank_table(per_ctx, stats, args, mode, world, dev) -> list:
+    """Every rank's (context's) timing and counted share, rank order: under torch.distributed one
+    all_gather_object; the in-process group holds every context's already."""
     import torch.distributed as dist
 
-    mine = [float(np.mean(x)) for x in per_ctx]
+    mine = [dict(t, rays=int(s["rays"]), algorithmic_bytes=int(algorithmic_bytes(s))) for t, s in zip(per_ctx, stats)]
     if mode != "dist" or world == 1:
-        return [round(v, 3) for v in mine]
-    t = torch.tensor(mine, dtype=torch.float64)
-    t = t.to(dev) if args.backend == "nccl" else t
-    parts = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(parts, t)
-    return [round(float(v), 3) for p in parts for v in p.cpu().tolist()]
+        return mine
+    parts = [None] * world
+    dist.all_gather_object(parts, mine)
+    return [r for p in parts for r in p]
+
+
+def per_rank_lines(table, workload, kname, global_mode) -> list:
+    """Per rank: its render (sample-kernel throughput ms per step), its part of the per-frame exchange,
+    and its roofline from the 1-GPU counters of the workload scaled by the rank's share of the counted
+    rays (a rank's launch does that share of the 1-GPU launch's work: its row bands of every frame)."""
+    total = sum(r["rays"] for r in table) or 1
+    out = []
+    for i, r in enumerate(table):
+        share = r["rays"] / total
+        rf = roofline(workload, r["kernel_ms"], r["algorithmic_bytes"], kname, global_mode=global_mode, scale=share)
+        out.append({"rank": i, "kernel_ms": round(r["kernel_ms"], 3), "launches_per_step": r["launches_per_step"],
+                    "exchange_ms": None if r["exchange_ms"] is None else round(r["exchange_ms"], 3),
+                    "rays_share": round(share, 5), "roofline": rf})
+    return out
 
 
 KERNEL_LDS = "srt::sample_kernel<false, true, true, 1024, false, false, 4> (LDS-resident scene)"
@@ -497,8 +546,8 @@ def main(argv=None):
     stream = torch.cuda.Stream(device=dev)   # a real (non-null) stream shared by torch and the library
     torch.cuda.set_stream(stream)
 
-    elapsed_s, total_rays, st, kernel_ms, run = run_leg(setup, spp, args, mode=mode, rank=rank, world=world,
-                                                        device=device, stream=stream)
+    elapsed_s, total_rays, st, per_ctx, run = run_leg(setup, spp, args, mode=mode, rank=rank, world=world,
+                                                      device=device, stream=stream)
     group_info = run.info() if mode == "group" else None  # (before a dump's radiance gather)
     if args.dump:
         fr = run.frame()
@@ -506,8 +555,9 @@ def main(argv=None):
             np.savez(args.dump, accum=fr[0], out=fr[1])
     kname = timed_kernel(run_compute(run), args.scene)
     par = parallelism(args, mode, world, run)
-    rk_ms = ranks_kernel_ms(kernel_ms, args, mode, world, dev)
+    table = rank_table(per_ctx, run.rank_stats() if mode == "group" else [st], args, mode, world, dev)
     run.close()
+    global_main = args.scene in ("synthetic", "torusknot")
 
     legs = []
     for leg, enabled, scene, lw, lh, lspp, ntri in (
@@ -516,30 +566,31 @@ def main(argv=None):
         if not enabled:
             continue
         lsetup, lname = build_setup(scene, lw, lh, lspp, 5, ntri)
-        l_el, l_rays, l_st, l_kms, l_run = run_leg(lsetup, lspp, args, mode=mode, rank=rank, world=world,
+        l_el, l_rays, l_st, l_ctx, l_run = run_leg(lsetup, lspp, args, mode=mode, rank=rank, world=world,
                                                    device=device, stream=stream)
         l_kname = timed_kernel(run_compute(l_run), scene)
-        l_rk = ranks_kernel_ms(l_kms, args, mode, world, dev)
+        l_table = rank_table(l_ctx, l_run.rank_stats() if mode == "group" else [l_st], args, mode, world, dev)
         l_run.close()
         if rank == 0:
             desc = (f"synthetic {ntri} triangles (SURVEY 8d generator)" if scene == "synthetic" else
                     "torus-knot tube, 262144 triangles (closed surface mesh; srt_amd.render.torus_knot_triangles), "
                     "model camera and lights")
+            l_ranks = per_rank_lines(l_table, lname, l_kname, True)
             legs.append({
                 "leg": leg, "workload": lname, "value": round(l_rays * args.steps / l_el / 1e6, 3),
                 "unit": "Mrays/s", "ms_per_step": round(l_el * 1e3 / args.steps, 3),
                 "config": {"scene": desc, "width": lw, "height": lh, "spp": lspp, "max_depth": 5},
-                "kernel_ms_per_rank": l_rk,
-                "roofline": roofline(lname, float(np.mean(l_kms[0])), algorithmic_bytes(l_st), l_kname,
-                                     global_mode=True) if world == 1 else
-                {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
-                 "kernel_ms": round(float(np.mean(l_kms[0])), 3), "note": "roofline reported at N=1"},
+                "kernel_ms_per_rank": [r["kernel_ms"] for r in l_ranks],
+                "exchange_ms_per_rank": [r["exchange_ms"] for r in l_ranks],
+                "roofline": max(l_ranks, key=lambda r: r["kernel_ms"])["roofline"],
+                "per_rank": l_ranks if world > 1 else None,
             })
 
     if rank == 0:
         ms_per_step = elapsed_s * 1e3 / args.steps
         value = total_rays * args.steps / elapsed_s / 1e6
-        k_ms = float(np.mean(kernel_ms[0]))
+        ranks = per_rank_lines(table, wl_name, kname, global_main)
+        slowest = max(ranks, key=lambda r: r["kernel_ms"])
         line = {
             "metric": "Mrays/s (CheckHit queries: camera + bounce + shadow rays) at the BASELINE frame/spp",
             "value": round(value, 3),
@@ -563,13 +614,15 @@ def main(argv=None):
             "msamples_per_s": round(W * H * spp * args.steps / elapsed_s / 1e6, 3),
             "rays_per_step": int(total_rays),
             "code_hash": code_hash(),
-            "kernel_ms_per_rank": rk_ms,
-            # per-rank counters describe one launch on one GPU: the roofline is a 1-GPU figure
-            "roofline": roofline(wl_name, k_ms, algorithmic_bytes(st), kname,
-                                 global_mode=args.scene in ("synthetic", "torusknot"))
-            if world == 1 else
-            {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
-             "kernel_ms": round(k_ms, 3), "note": "roofline reported at N=1"},
+            # sample-kernel throughput time per step of every rank (launches overlap their predecessor's
+            # drain: each counts from its start or the previous launch's end to its end, srt_kernel_time),
+            # and each rank's part of the per-frame sRGB8 exchange (N > 1)
+            "kernel_ms_per_rank": [r["kernel_ms"] for r in ranks],
+            "exchange_ms_per_rank": [r["exchange_ms"] for r in ranks],
+            "launch_overlap": all(r["overlap"] for r in table),
+            # the step's bound: the slowest rank's launch, its counters the 1-GPU launch's scaled by its share
+            "roofline": slowest["roofline"],
+            "per_rank": ranks if world > 1 else None,
             "legs": legs,
         }
         if group_info is not None:

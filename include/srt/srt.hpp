@@ -231,6 +231,20 @@ class ComputeGroup {
     check(srt_group_last_kernel_ms(group(), v.data(), (int)v.size()), "ComputeGroup::KernelMs");
     return v;
   }
+  // per device since the last call: sample-kernel throughput ms (back-to-back frames read once), and the
+  // ms of its part of the per-frame sRGB8 exchange (device 0's includes the assembly)
+  std::vector<double> KernelTime() {
+    std::vector<double> v(parts_.size());
+    std::vector<int> n(parts_.size());
+    check(srt_group_kernel_time(group(), v.data(), n.data(), (int)v.size()), "ComputeGroup::KernelTime");
+    return v;
+  }
+  std::vector<double> ExchangeTime() {
+    std::vector<double> v(parts_.size());
+    std::vector<int> n(parts_.size());
+    check(srt_group_exchange_time(group(), v.data(), n.data(), (int)v.size()), "ComputeGroup::ExchangeTime");
+    return v;
+  }
 
   void SetBool(const std::string& n, bool v) { ForEach([&](Compute& c) { c.SetBool(n, v); }); }
   void SetInt(const std::string& n, int v) {

@@ -122,15 +122,21 @@ int srt_finish(srt_context* ctx);
  * uniform at frame_first + nframes - 1, as the last dispatch would. */
 int srt_render_frames(srt_context* ctx, int frame_first, int nframes, int write_output, int count);
 int srt_get_stats(srt_context* ctx, srt_stats* out);
-/* Device time of the path-tracing kernel launches of the last render call:
- * each sample_kernel / sphere_kernel launch's span from its first wave's start
- * to its last wave's end (the GPU's 100 MHz real-time clock; a pipelined launch
- * overlaps its neighbours, which HIP events around it would count), and HIP
- * events around pool and wavefront launches.  Waits for the render. */
+/* Device time of the path-tracing kernel launches of the last render call,
+ * from each sample_kernel / sphere_kernel launch's span (its first wave's start
+ * to its last wave's end on the GPU's 100 MHz real-time clock): a launch counts
+ * from its start, or from the end of the context's launch before it when that
+ * is later, to its end -- its span when launches run in series, the interval
+ * between consecutive launch ends when overlapped pipeline slots start it while
+ * its predecessor drains (HIP events or rocprofv3's dispatch-to-end time would
+ * also count its wait for the CUs).  HIP events around pool and wavefront
+ * launches.  Waits for the render. */
 int srt_last_kernel_ms(srt_context* ctx, float* ms);
-/* The summed spans of every sample_kernel / sphere_kernel launch since the
- * previous call (at most the last 1024), and how many: a timed loop of renders
- * enqueued without synchronising reads its kernel time once.  Waits for them. */
+/* The same throughput time summed over every sample_kernel / sphere_kernel
+ * launch since the previous call, and how many: a timed loop of renders
+ * enqueued without synchronising reads its kernel time once.  Waits for them.
+ * SRT_ERR_LIMIT when more than 4096 launches went unread (their records are
+ * overwritten): the total would cover only part of them. */
 int srt_kernel_time(srt_context* ctx, double* total_ms, int* launches);
 int srt_reset_stats(srt_context* ctx);  /* also zeroes the NaN counter */
 /* Failure detection: path samples with a NaN component accumulated since the
@@ -149,7 +155,9 @@ int srt_local_rows(srt_context* ctx);
  * uploaded scene's size chose for global-scene mode's timed kernel: "scene.fused" (1: fused
  * sub-steps, 0: the IL pattern), "scene.global_waves" (waves per SIMD of the fused instance) and
  * "scene.tri_slots" (device triangle records: more than the scene's triangles when small leaves
- * are laid out line by line for a tree streamed from HBM). */
+ * are laid out line by line for a tree streamed from HBM); and of the last render call,
+ * "launch.chunks" (its sample launches: one per sample-buffer chunk) and "launch.overlap" (1 when
+ * its launches may start while the previous one drains, SRT_PIPELINE_OVERLAP). */
 int srt_device(srt_context* ctx);
 int srt_get_int(srt_context* ctx, const char* name, int* v);
 
@@ -166,8 +174,10 @@ int srt_get_int(srt_context* ctx, const char* name, int* v);
  * accumulation image is asked for (srt_group_read_accum, srt_group_image_pointers' accum_dev).
  * The frame is bit-identical to one device's.  A device list that repeats a device (RCCL takes one rank
  * per device), or SRT_GROUP_TRANSPORT=copy, gathers with device-to-device copies instead.
- * Contexts stay owned by the caller and must outlive the group; srt_group_destroy gives each back
- * its own full-frame images (tiling rank 0 of 1), so they can be dispatched again. */
+ * Contexts stay owned by the caller and must outlive the group; srt_group_destroy detaches each from
+ * the freed band images without allocating (tiling rank 0 of 1, no images: a dispatch returns
+ * SRT_ERR_STATE until srt_alloc_images or srt_set_image_buffers gives it images again).
+ * srt_group_create fails (SRT_ERR_HIP) unless every RCCL communicator counts exactly n ranks. */
 typedef struct srt_group srt_group;
 int srt_group_create(srt_context* const* ctxs, int n, int band_rows, srt_group** out);
 int srt_group_destroy(srt_group* g);
@@ -177,6 +187,15 @@ int srt_group_destroy(srt_group* g);
 int srt_group_get_int(srt_group* g, const char* name, int* v);
 /* Each context's srt_last_kernel_ms (its sample launches' spans), n entries. */
 int srt_group_last_kernel_ms(srt_group* g, float* ms, int n);
+/* Each context's srt_kernel_time since the previous call (n entries each): a timed loop of group
+ * renders enqueued back to back reads every device's kernel time once, after it. */
+int srt_group_kernel_time(srt_group* g, double* total_ms, int* launches, int n);
+/* Each context's part of the per-frame exchange since the previous call (n entries each), from HIP
+ * events on its gather stream: from the frame's own rows being rendered to the end of its part of
+ * the gather (the RCCL gather waits for every rank; copies for context 0's buffer), and for context
+ * 0 to the end of the frame's assembly (the de-interleave); summed, with the frame count.
+ * SRT_ERR_LIMIT when more than 4096 frames went unread. */
+int srt_group_exchange_time(srt_group* g, double* total_ms, int* frames, int n);
 /* Uniform setters broadcast to every context (the names of srt_set_*). */
 int srt_group_set_bool(srt_group* g, const char* name, int v);
 int srt_group_set_int(srt_group* g, const char* name, int v);

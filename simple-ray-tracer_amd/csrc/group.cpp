@@ -162,6 +162,11 @@ struct srt_group {
   std::vector<hipEvent_t> acc_sent;  // per context: the radiance gather that read its accumulation image
   std::vector<hipEvent_t> arrived;   // per context, copy transport: its rows are in context 0's buffer
   hipEvent_t assembled = nullptr;    // context 0's gather stream: the last assembly (it read recv_*)
+  // per context: timing events around its part of each frame's exchange (srt_group_exchange_time), a
+  // ring of kExCap pairs created as they are first used; ex_seq frames recorded, ex_read summed
+  static constexpr int kExCap = 4096;
+  std::vector<std::vector<hipEvent_t>> ex_ev;
+  long long ex_seq = 0, ex_read = 0;
   int band_rows = 8;
   int W = 0, H = 0, rows_pad = 0;
   int cur = 0;               // the sRGB8 buffer the next frame writes
@@ -218,6 +223,12 @@ void DestroyStreamsEvents(srt_group* g) {
     }
     v.clear();
   };
+  for (size_t i = 0; i < g->ex_ev.size(); ++i) {  // context i's exchange timing events, on its device
+    (void)hipSetDevice(g->dev[i]);
+    for (hipEvent_t e : g->ex_ev[i])
+      if (e) (void)hipEventDestroy(e);
+  }
+  g->ex_ev.clear();
   destroy(g->rendered);
   destroy(g->sent[0]);
   destroy(g->sent[1]);
@@ -267,12 +278,30 @@ int PrepareLaunch(srt_group* g, int i, int b) {
 // One gather of every context's `bytes` at send[i] into context 0's `recv` (rank order), on the
 // gather streams, behind each context's launches so far; `sent_ev[i]` marks the end of context i's
 // part (its send buffer may be written again after it).
-int Gather(srt_group* g, const std::vector<void*>& send, void* recv, size_t bytes, std::vector<hipEvent_t>& sent_ev) {
+// Timing event `k` (0: start, 1: end) of context i's part of exchange frame g->ex_seq, created on first use.
+int ExEvent(srt_group* g, int i, int k, hipEvent_t* out) {
+  auto& v = g->ex_ev[i];
+  const size_t at = 2 * (size_t)(g->ex_seq % srt_group::kExCap) + k;
+  if (v.size() <= at) v.resize(at + 1, nullptr);
+  if (!v[at]) GHIP(hipEventCreate(&v[at]));  // (the caller has set context i's device)
+  *out = v[at];
+  return SRT_OK;
+}
+
+// `timed`: the per-frame exchange, whose parts srt_group_exchange_time reports.
+int Gather(srt_group* g, const std::vector<void*>& send, void* recv, size_t bytes, std::vector<hipEvent_t>& sent_ev,
+           bool timed) {
   const int n = (int)g->ctx.size();
+  if (timed && g->ex_ev.size() != (size_t)n) g->ex_ev.resize(n);
   for (int i = 0; i < n; ++i) {
     GHIP(hipSetDevice(g->dev[i]));
     GHIP(hipEventRecord(g->rendered[i], g->stream[i]));
     GHIP(hipStreamWaitEvent(g->xfer[i], g->rendered[i], 0));
+    if (timed) {
+      hipEvent_t e;
+      if (int rc = ExEvent(g, i, 0, &e)) return rc;
+      GHIP(hipEventRecord(e, g->xfer[i]));
+    }
   }
   if (!g->comm.empty()) {
     const Rccl& R = rccl();
@@ -297,6 +326,11 @@ int Gather(srt_group* g, const std::vector<void*>& send, void* recv, size_t byte
   for (int i = 0; i < n; ++i) {
     GHIP(hipSetDevice(g->dev[i]));
     GHIP(hipEventRecord(sent_ev[i], g->xfer[i]));
+    if (timed && i > 0) {  // (context 0's part ends after the assembly, GatherOutput)
+      hipEvent_t e;
+      if (int rc = ExEvent(g, i, 1, &e)) return rc;
+      GHIP(hipEventRecord(e, g->xfer[i]));
+    }
   }
   GHIP(hipSetDevice(g->dev[0]));
   return SRT_OK;
@@ -306,11 +340,15 @@ int Gather(srt_group* g, const std::vector<void*>& send, void* recv, size_t byte
 // dispatch extent.
 int GatherOutput(srt_group* g, int b, int ext_w, int ext_h) {
   const size_t bytes = (size_t)g->rows_pad * g->W * 4;
-  if (int rc = Gather(g, g->band_out[b], g->recv_out, bytes, g->sent[b])) return rc;
+  if (int rc = Gather(g, g->band_out[b], g->recv_out, bytes, g->sent[b], true)) return rc;
   if (int rc = srt::AssembleOutputOn(g->ctx[0], g->xfer[0], g->recv_out, (int)g->ctx.size(), g->rows_pad,
                                      g->band_rows, ext_w, ext_h, g->full_out))
     return rc;
   GHIP(hipEventRecord(g->assembled, g->xfer[0]));
+  hipEvent_t e;
+  if (int rc = ExEvent(g, 0, 1, &e)) return rc;
+  GHIP(hipEventRecord(e, g->xfer[0]));
+  ++g->ex_seq;
   ++g->gathers_out;
   return SRT_OK;
 }
@@ -324,7 +362,7 @@ int GatherAccum(srt_group* g) {
     GHIP(hipSetDevice(g->dev[0]));
     GHIP(hipMalloc(&g->recv_acc, (size_t)n * bytes));
   }
-  if (int rc = Gather(g, g->band_accum, g->recv_acc, bytes, g->acc_sent)) return rc;
+  if (int rc = Gather(g, g->band_accum, g->recv_acc, bytes, g->acc_sent, false)) return rc;
   if (int rc = srt::AssembleBandsOn(g->ctx[0], g->xfer[0], g->recv_acc, n, g->rows_pad, g->band_rows, 1,
                                     g->full_accum, nullptr))
     return rc;
@@ -332,6 +370,15 @@ int GatherAccum(srt_group* g) {
   ++g->gathers_acc;
   g->accum_stale = false;
   return SRT_OK;
+}
+
+// A frame some contexts enqueued and others failed to: the contexts' radiance may have moved, so the
+// assembled copy is stale, and everything in flight is drained (no gather may still read a buffer the
+// next frame writes).  Returns the frame's error.
+int Abandon(srt_group* g, int rc) {
+  g->accum_stale = true;
+  (void)srt_group_finish(g);
+  return rc;
 }
 
 }  // namespace
@@ -371,6 +418,18 @@ int srt_group_create(srt_context* const* ctxs, int n, int band_rows, srt_group**
       delete g;
       return SRT_ERR_HIP;
     }
+    for (int i = 0; i < n; ++i) {  // every communicator must see all n ranks, or the gather is not the frame
+      int count = 0;
+      const ncclResult_t rc = R.CommCount(g->comm[i], &count);
+      if (rc != ncclSuccess || count != n) {
+        srt::SetError("group: ncclCommCount of communicator " + std::to_string(i) + " is " + std::to_string(count) +
+                      ", not the group's " + std::to_string(n) + " ranks");
+        for (ncclComm_t cm : g->comm) (void)R.CommDestroy(cm);
+        g->comm.clear();
+        delete g;
+        return SRT_ERR_HIP;
+      }
+    }
   }
   if (int rc = CreateStreamsEvents(g)) {
     srt_group_destroy(g);
@@ -386,13 +445,10 @@ int srt_group_destroy(srt_group* g) {
   if (!g) return SRT_ERR_INVALID;
   g->workers.reset();
   (void)srt_group_finish(g);
-  // the contexts outlive the group: give each its own full-frame images back (and tiling 0 of 1), so
-  // that no context keeps a pointer to the band images freed below
+  // the contexts outlive the group: detach each from the band images freed below (rank 0 of 1, no
+  // images; nothing is allocated here -- the caller gives a context images again before dispatching it)
   if (!g->band_accum.empty())
-    for (srt_context* c : g->ctx) {
-      (void)srt_set_tiling(c, 0, 1, g->band_rows);
-      (void)srt_alloc_images(c);
-    }
+    for (srt_context* c : g->ctx) (void)srt::DetachImages(c);
   FreeImages(g);
   if (!g->comm.empty())
     for (ncclComm_t c : g->comm) (void)rccl().CommDestroy(c);
@@ -434,6 +490,44 @@ int srt_group_last_kernel_ms(srt_group* g, float* ms, int n) {
   if (!g || !ms || n < 0) return SRT_ERR_INVALID;
   for (int i = 0; i < n && i < (int)g->ctx.size(); ++i)
     if (int rc = srt_last_kernel_ms(g->ctx[i], ms + i)) return rc;
+  return SRT_OK;
+}
+
+int srt_group_kernel_time(srt_group* g, double* total_ms, int* launches, int n) {
+  if (!g || !total_ms || !launches || n < 0) return SRT_ERR_INVALID;
+  int first = SRT_OK;
+  for (int i = 0; i < n && i < (int)g->ctx.size(); ++i) {  // (every context's records are consumed)
+    const int rc = srt_kernel_time(g->ctx[i], total_ms + i, launches + i);
+    if (rc && !first) first = rc;
+  }
+  return first;
+}
+
+int srt_group_exchange_time(srt_group* g, double* total_ms, int* frames, int n) {
+  if (!g || !total_ms || !frames || n < 0) return SRT_ERR_INVALID;
+  const int m = std::min(n, (int)g->ctx.size());
+  for (int i = 0; i < m; ++i) total_ms[i] = 0.0, frames[i] = 0;
+  for (size_t i = 0; i < g->xfer.size(); ++i) {
+    GHIP(hipSetDevice(g->dev[i]));
+    GHIP(hipStreamSynchronize(g->xfer[i]));
+  }
+  const long long from = g->ex_read;
+  g->ex_read = g->ex_seq;
+  if (g->ex_seq - from > srt_group::kExCap) {
+    srt::SetError("srt_group_exchange_time: more than 4096 frames since the last call (timing events reused)");
+    return SRT_ERR_LIMIT;
+  }
+  for (int i = 0; i < m && i < (int)g->ex_ev.size(); ++i) {
+    GHIP(hipSetDevice(g->dev[i]));
+    for (long long q = from; q < g->ex_seq; ++q) {
+      const size_t at = 2 * (size_t)(q % srt_group::kExCap);
+      float t = 0.0f;
+      GHIP(hipEventElapsedTime(&t, g->ex_ev[i][at], g->ex_ev[i][at + 1]));
+      total_ms[i] += t;
+      ++frames[i];
+    }
+  }
+  GHIP(hipSetDevice(g->dev[0]));
   return SRT_OK;
 }
 
@@ -515,7 +609,7 @@ int srt_group_dispatch(srt_group* g, uint32_t gx, uint32_t gy) {
         if (int r = PrepareLaunch(g, i, b)) return r;
         return srt_dispatch(g->ctx[i], gx, gy);
       }))
-    return rc;
+    return Abandon(g, rc);
   g->accum_stale = true;
   int reset = 0;
   srt_get_int(g->ctx[0], "resetAccumBuffer", &reset);
@@ -536,7 +630,7 @@ int srt_group_render_frames(srt_group* g, int frame_first, int nframes) {
         if (int r = PrepareLaunch(g, i, b)) return r;
         return srt_render_frames(g->ctx[i], frame_first, nframes, 1, 0);
       }))
-    return rc;
+    return Abandon(g, rc);
   g->accum_stale = true;
   const int rc = GatherOutput(g, g->cur, g->W, g->H);
   g->cur ^= 1;

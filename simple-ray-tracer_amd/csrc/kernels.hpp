@@ -582,7 +582,7 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
 
 // A mesh scene (showModel set); FUSE/GW: global-scene mode's schedule and waves per SIMD.
 template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX, bool FUSE, int GW = 4>
-__global__ __launch_bounds__(BLOCK, LDSM ? 4 : GW) void sample_kernel(KParams kp) {
+__global__ __launch_bounds__(BLOCK, LDSM ? BLOCK / 256 : GW) void sample_kernel(KParams kp) {
   sample_body<COUNT, LDSM, PACK, BLOCK, TEX, FUSE, GW, false>(kp);
 }
 

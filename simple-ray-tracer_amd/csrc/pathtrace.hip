@@ -131,7 +131,9 @@ struct srt_context {
   unsigned long long* d_batch_ctr = nullptr;  // one batch counter per chunk launch
   int batch_ctr_cap = 0;
   size_t lbuf_bytes = 0;
-  size_t lbuf_cap = (size_t)16 << 30;  // SRT_SAMPLE_BUFFER_MB
+  // SRT_SAMPLE_BUFFER_MB: every sample buffer of the context together (its own, used by counting and
+  // unpipelined launches, and one per pipeline slot), split equally: 16 GiB each with the 3 default slots
+  size_t lbuf_total = (size_t)64 << 30;
   int tail_claims = 16;  // SRT_TAIL_CLAIMS: claims per wave before the end from which claims take one batch
   int tail_claims_sph = 1;  // the sphere launch's (C2, 8 per claim: tail 16 6.20 ms, 1 3.17 ms; its batches
                             // are cheap, the counter's atomic rate bounds it); SRT_TAIL_CLAIMS sets both
@@ -213,11 +215,13 @@ struct srt_context {
   };
   std::vector<Slot> slots;
   int pipe = 3;                    // SRT_PIPELINE
-  // SRT_PIPELINE_OVERLAP: whether a sample launch may start before the previous one ends (2: always; 1, the
-  // default: on a rank's share of a multi-GPU split (nranks > 1), whose short launches lose ~3% to the
-  // drain; 0: never).  An overlapped launch's dispatch-to-end time (rocprofv3) and span include its wait
-  // for the CUs its predecessor still holds, so the 1-GPU launch the roofline is quoted on runs serially.
-  int pipe_overlap = 1;
+  // SRT_PIPELINE_OVERLAP: whether a sample launch may start before the previous one ends (2, the default:
+  // always; 1: on a rank's share of a multi-GPU split (nranks > 1) only; 0: never).  An overlapped launch's
+  // dispatch-to-end time (rocprofv3) and span include its wait for the CUs its predecessor still holds, so
+  // kernel time is a throughput time: each launch counts from its start or its predecessor's end, whichever
+  // is later, to its end (srt_kernel_time; tools/trace_intervals.py applies the same rule to rocprofv3's
+  // kernel trace).
+  int pipe_overlap = 2;
   hipEvent_t last_sampled = nullptr;  // the last sample launch's end (a slot's `sampled`, or plain_done)
   hipEvent_t plain_done = nullptr;    // recorded on `stream` after a launch outside the slots
   unsigned long long pipe_seq = 0;
@@ -226,7 +230,7 @@ struct srt_context {
   // last wave's end; s_memrealtime) into a record of this ring (HIP events around a pipelined launch
   // would also time its wait for the CUs its predecessor still holds).
   unsigned long long* d_span = nullptr;
-  static constexpr int kSpanCap = 1024;
+  static constexpr int kSpanCap = 4096;
   unsigned long long span_seq = 0, span_read = 0;  // records written / summed by srt_kernel_time
   std::vector<long long> chunk_span;               // per chunk of the last render: its record (or -1)
   hipEvent_t lidle = nullptr;      // synchronized before the current launch frees a launch buffer
@@ -473,6 +477,12 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
 
 // LDS budget per CU (gfx950: 160 KiB; one 1024-thread block per CU in LDS mode)
 constexpr size_t kLdsBytes = 160 * 1024;
+// LDS mode's block (one per CU, the scene copied into its LDS): 1024 threads = 4 waves per SIMD.  An
+// experiment build with 768 (3 waves per SIMD) measures what a wave per SIMD is worth
+#ifndef SRT_LDS_BLOCK
+#define SRT_LDS_BLOCK 1024
+#endif
+constexpr int kLdsBlock = SRT_LDS_BLOCK;
 
 template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX, bool FUSE = false, int GW = 4>
 int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
@@ -575,10 +585,10 @@ int LaunchSpheres(srt_context* c, srt::KParams kp, size_t lds) {
 template <bool TEX>
 int LaunchMode(srt_context* c, const srt::KParams& kc, size_t lds, bool count, bool ldsm, bool pack) {
   if (!kc.show_model) return count ? LaunchSpheres<true>(c, kc, lds) : LaunchSpheres<false>(c, kc, lds);
-  if (count && ldsm) return LaunchSamples<true, true, true, 1024, TEX>(c, kc, lds);
+  if (count && ldsm) return LaunchSamples<true, true, true, kLdsBlock, TEX>(c, kc, lds);
   if (count) return pack ? LaunchSamples<true, false, true, 256, TEX>(c, kc, lds)
                          : LaunchSamples<true, false, false, 256, TEX>(c, kc, lds);
-  if (ldsm) return LaunchSamples<false, true, true, 1024, TEX>(c, kc, lds);
+  if (ldsm) return LaunchSamples<false, true, true, kLdsBlock, TEX>(c, kc, lds);
   if (c->fused && c->global_waves == 5) return pack ? LaunchSamples<false, false, true, 256, TEX, true, 5>(c, kc, lds)
                                                    : LaunchSamples<false, false, false, 256, TEX, true, 5>(c, kc, lds);
   if (c->fused) return pack ? LaunchSamples<false, false, true, 256, TEX, true>(c, kc, lds)
@@ -830,9 +840,9 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   // LDS mode: the whole scene + 1024 lanes' 2-dword stacks fit in one CU's LDS
   // (node pairs at the padded LDS stride; only for node arrays whose pairs are all 64-B aligned)
   const size_t scene_bytes = ((size_t)kp.nodes_lds_f4 + (size_t)kp.tris_f4) * sizeof(float4);
-  const size_t lds_mode_bytes = scene_bytes + (size_t)1024 * 2 * sizeof(uint32_t) * (size_t)kp.stack_entries;
+  const size_t lds_mode_bytes = scene_bytes + (size_t)kLdsBlock * 2 * sizeof(uint32_t) * (size_t)kp.stack_entries;
   const bool ldsm = kp.show_model && c->lds_ok && c->pairs_aligned && !c->force_global && lds_mode_bytes <= kLdsBytes;
-  const int block = ldsm ? 1024 : 256;
+  const int block = ldsm ? kLdsBlock : 256;
   // pool mode (pool.hpp): LDS mode with stacks for the traversal waves only, then the ray records;
   // laid out first, and sample_kernel's layout when the records do not fit
   bool pool = ldsm && c->pool && !c->sample_textures && kp.max_depth >= 0 && kp.max_depth <= 255;
@@ -905,8 +915,10 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   const bool wf = !ldsm && !count && kp.show_model && (c->wavefront >= 0 ? c->wavefront == 1 : c->wf_scene);
   const size_t max_frames = std::max<size_t>(
       1, ((size_t)0x7FFFFFFF - ((size_t)1 << 20)) / std::max<size_t>(1, n_tiles) / (wf ? 64 : 1));
+  // the context's sample buffers share SRT_SAMPLE_BUFFER_MB: its own and, with pipeline slots, one per slot
+  const size_t lbuf_cap = c->lbuf_total / (size_t)(c->pipe > 1 ? c->pipe + 1 : 1);
   const int chunk = (int)std::max<size_t>(
-      1, std::min<size_t>(std::min<size_t>((size_t)kp.nframes, max_frames), c->lbuf_cap / per_frame));
+      1, std::min<size_t>(std::min<size_t>((size_t)kp.nframes, max_frames), lbuf_cap / per_frame));
   const size_t need = per_frame * (size_t)chunk;
   const bool piped = !count && !pool && !wf && c->pipe > 1;
   // (a counting launch, the untimed first launch of a measurement, sets the slots up for the timed ones)
@@ -1262,6 +1274,21 @@ int AssembleOutputOn(srt_context* c, void* stream, const void* gathered_rgba8, i
   return SRT_OK;
 }
 
+int DetachImages(srt_context* c) {
+  if (!c) return SRT_ERR_INVALID;
+  HIP_OK(hipSetDevice(c->device));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  if (int rq = Quiesce(c)) return rq;
+  if (!c->images_external) { FreeDev(c->d_accum); FreeDev(c->d_out); }
+  c->d_accum = nullptr;
+  c->d_out = nullptr;
+  c->images_external = false;
+  c->img_w = c->img_rows = 0;
+  c->rank = 0;
+  c->nranks = 1;
+  return SRT_OK;
+}
+
 }  // namespace srt
 
 // ===========================================================================
@@ -1282,8 +1309,8 @@ int srt_create(int device, void* stream, srt_context** out) {
   auto* c = new srt_context();
   c->device = device;
   if (const char* e = std::getenv("SRT_FORCE_GLOBAL_SCENE")) c->force_global = e[0] == '1';
-  if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_MB")) c->lbuf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
-  if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_KB")) c->lbuf_cap = (size_t)std::max(1L, std::atol(e)) << 10;
+  if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_MB")) c->lbuf_total = (size_t)std::max(1L, std::atol(e)) << 20;
+  if (const char* e = std::getenv("SRT_SAMPLE_BUFFER_KB")) c->lbuf_total = (size_t)std::max(1L, std::atol(e)) << 10;
   if (const char* e = std::getenv("SRT_BOUNCE_CAP")) c->bounce_cap = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("SRT_POOL")) c->pool = e[0] == '1';
   if (const char* e = std::getenv("SRT_POOL_BATCH")) c->pool_batch = std::max(1, std::min(64, std::atoi(e)));
@@ -1448,6 +1475,8 @@ int srt_get_int(srt_context* c, const char* name, int* v) {
   else if (n == "scene.wf_waves") *v = c->wf_waves;
   else if (n == "scene.treelets") *v = (int)c->n_treelets;
   else if (n == "scene.tri_slots") *v = (int)c->n_tris;  // device triangle records (LayoutTris gaps included)
+  else if (n == "launch.chunks") *v = c->ev_used / 2;   // sample launches of the last render or dispatch
+  else if (n == "launch.overlap") *v = (c->pipe > 1 && (c->pipe_overlap == 2 || (c->pipe_overlap == 1 && c->nranks > 1))) ? 1 : 0;
   else return SRT_ERR_NOT_FOUND;
   return SRT_OK;
 }
@@ -1529,18 +1558,45 @@ extern "C" int srt_debug_wave_trace(srt_context* c, unsigned long long* out, int
 }
 #endif
 
+// Kernel time of sample launches from their span records (first wave's start, last wave's end; 100 MHz
+// ticks).  Launch q counts from its start, or from the end of launch q - 1 (the context's launch before it)
+// when that is later, to its end: its own span when launches run in series, the interval between
+// consecutive launch ends when a launch is dispatched while its predecessor drains (overlapped pipeline
+// slots, whose spans include the wait for the CUs the predecessor still holds).  The sum over launches is
+// the time during which some sample launch of the context runs.
+namespace {
+bool SpanRecord(const srt_context* c, const unsigned long long* ring, unsigned long long q, unsigned long long* t0,
+                unsigned long long* t1) {
+  if (q >= c->span_seq || q + srt_context::kSpanCap < c->span_seq) return false;  // not written, or overwritten
+  const unsigned long long* sp = ring + 2 * (q % srt_context::kSpanCap);
+  if (sp[1] < sp[0]) return false;
+  *t0 = sp[0];
+  *t1 = sp[1];
+  return true;
+}
+double SpanCreditMs(const srt_context* c, const unsigned long long* ring, unsigned long long q) {
+  unsigned long long t0, t1, p0, p1;
+  if (!SpanRecord(c, ring, q, &t0, &t1)) return 0.0;
+  if (q > 0 && SpanRecord(c, ring, q - 1, &p0, &p1) && p1 > t0) t0 = std::min(p1, t1);
+  return (double)(t1 - t0) * 1e-5;
+}
+}  // namespace
+
 int srt_last_kernel_ms(srt_context* c, float* ms) {
   if (!c || !ms) return SRT_ERR_INVALID;
   *ms = 0.0f;
+  std::vector<unsigned long long> ring;
   for (int i = 0; i + 1 < c->ev_used; i += 2) {
     HIP_OK(hipEventSynchronize(c->ev[i + 1]));
     const size_t chunk = (size_t)(i / 2);
     const long long rec = chunk < c->chunk_span.size() ? c->chunk_span[chunk] : -1;
     if (rec >= 0 && (unsigned long long)rec + srt_context::kSpanCap >= c->span_seq) {  // the launch's own span
-      unsigned long long sp[2];
-      HIP_OK(hipMemcpy(sp, c->d_span + 2 * ((unsigned long long)rec % srt_context::kSpanCap), sizeof sp,
-                       hipMemcpyDeviceToHost));
-      if (sp[1] >= sp[0]) *ms += (float)((double)(sp[1] - sp[0]) * 1e-5);  // 100 MHz ticks
+      if (ring.empty()) {
+        if (int rq = Quiesce(c)) return rq;  // (the launch before the render's first may be another slot's)
+        ring.resize(2 * srt_context::kSpanCap);
+        HIP_OK(hipMemcpy(ring.data(), c->d_span, sizeof(unsigned long long) * ring.size(), hipMemcpyDeviceToHost));
+      }
+      *ms += (float)SpanCreditMs(c, ring.data(), (unsigned long long)rec);
       continue;
     }
     float t = 0.0f;  // pool and wavefront launches: the HIP events around them
@@ -1556,18 +1612,20 @@ int srt_kernel_time(srt_context* c, double* total_ms, int* launches) {
   *launches = 0;
   HIP_OK(hipStreamSynchronize(c->stream));
   if (int rq = Quiesce(c)) return rq;
-  unsigned long long from = c->span_read;
-  if (c->span_seq - from > (unsigned long long)srt_context::kSpanCap) from = c->span_seq - srt_context::kSpanCap;
+  const unsigned long long from = c->span_read;
+  c->span_read = c->span_seq;
+  if (c->span_seq - from > (unsigned long long)srt_context::kSpanCap) {  // records were overwritten unread
+    srt::SetError("srt_kernel_time: more than 4096 sample launches since the last call (span records lost)");
+    return SRT_ERR_LIMIT;
+  }
   if (c->span_seq > from) {
-    std::vector<unsigned long long> all(2 * srt_context::kSpanCap);
-    HIP_OK(hipMemcpy(all.data(), c->d_span, sizeof(unsigned long long) * all.size(), hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> ring(2 * srt_context::kSpanCap);
+    HIP_OK(hipMemcpy(ring.data(), c->d_span, sizeof(unsigned long long) * ring.size(), hipMemcpyDeviceToHost));
     for (unsigned long long q = from; q < c->span_seq; ++q) {
-      const unsigned long long* sp = &all[2 * (q % srt_context::kSpanCap)];
-      if (sp[1] >= sp[0]) *total_ms += (double)(sp[1] - sp[0]) * 1e-5;
+      *total_ms += SpanCreditMs(c, ring.data(), q);
       ++*launches;
     }
   }
-  c->span_read = c->span_seq;
   return SRT_OK;
 }
 

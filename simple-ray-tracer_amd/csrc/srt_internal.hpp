@@ -132,5 +132,8 @@ int AssembleBandsOn(srt_context* c, void* stream, const void* gathered, int nran
                     int frames, void* accum_full, void* out_full);
 int AssembleOutputOn(srt_context* c, void* stream, const void* gathered_rgba8, int nranks, int rows_pad,
                      int band_rows, int ext_w, int ext_h, void* out_full);
+// pathtrace.hip: a context leaves a device group without allocating: rank 0 of 1, no images (a
+// dispatch returns SRT_ERR_STATE until it is given images again)
+int DetachImages(srt_context* c);
 
 }  // namespace srt

@@ -127,6 +127,8 @@ _SIGS = {
     "srt_group_transport": (C.c_char_p, [P]),
     "srt_group_get_int": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_int)]),
     "srt_group_last_kernel_ms": (C.c_int, [P, C.POINTER(C.c_float), C.c_int]),
+    "srt_group_kernel_time": (C.c_int, [P, C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_int]),
+    "srt_group_exchange_time": (C.c_int, [P, C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_int]),
     "srt_upload_scene": (C.c_int, [P, P, C.c_uint32, P, C.c_uint32, P, P, C.c_uint32, P, C.c_uint32, P,
                                    C.c_uint32]),
     "srt_upload_textures": (C.c_int, [P, C.POINTER(Texture), C.c_uint32]),

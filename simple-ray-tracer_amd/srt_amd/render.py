@@ -163,6 +163,30 @@ class GroupRenderer:
         check(lib().srt_group_last_kernel_ms(self.g, ms, len(self.parts)), "group_last_kernel_ms")
         return [float(x) for x in ms]
 
+    def kernel_time(self) -> list[tuple[float, int]]:
+        """Each context's (sample-kernel throughput ms, launches) since the previous call
+        (srt_group_kernel_time): a timed loop of group renders enqueued back to back reads it once."""
+        import ctypes as C
+
+        from ._lib import check, lib
+
+        n = len(self.parts)
+        ms, k = (C.c_double * n)(), (C.c_int * n)()
+        check(lib().srt_group_kernel_time(self.g, ms, k, n), "group_kernel_time")
+        return [(float(ms[i]), int(k[i])) for i in range(n)]
+
+    def exchange_time(self) -> list[tuple[float, int]]:
+        """Each context's (ms in its part of the per-frame sRGB8 exchange, frames) since the previous call
+        (srt_group_exchange_time; context 0's part includes the assembly)."""
+        import ctypes as C
+
+        from ._lib import check, lib
+
+        n = len(self.parts)
+        ms, k = (C.c_double * n)(), (C.c_int * n)()
+        check(lib().srt_group_exchange_time(self.g, ms, k, n), "group_exchange_time")
+        return [(float(ms[i]), int(k[i])) for i in range(n)]
+
     def count(self, spp: int) -> dict:
         """Untimed counting render (the counting instance on every context, CheckHit counts summed) of
         the reset frame + `spp` frames.  The contexts' radiance is left at the rendered frame; the group's
@@ -174,8 +198,9 @@ class GroupRenderer:
         self.accum_frames = spp + 1
         self.finish()
         tot: dict = {}
-        for p in self.parts:
-            for k, v in p.compute.stats().items():
+        self.part_stats = [p.compute.stats() for p in self.parts]  # each context's share of the counts
+        for st in self.part_stats:
+            for k, v in st.items():
                 tot[k] = max(tot.get(k, 0), v) if k == "max_stack" else tot.get(k, 0) + v
         return tot
 
@@ -272,10 +297,8 @@ def synthetic_triangles(n_tris: int, seed: int = 0x5EED2025) -> np.ndarray:
     return tri.reshape(n_tris, 9)
 
 
-def torus_knot_triangles(n_u: int = 512, n_v: int = 256, p: int = 2, q: int = 3) -> np.ndarray:
-    """A closed surface mesh for the global-scene path (the Airplane OBJ is absent): a (p, q) torus-knot tube,
-    2 * n_u * n_v triangles, centred at (0, 9, 0) in the Rubik's extent (~18 units across) so the model camera
-    and lights of src/main.cpp frame it.  Deterministic (float64 numpy, rounded once to float32)."""
+def torus_knot_grid(n_u: int = 512, n_v: int = 256, p: int = 2, q: int = 3) -> np.ndarray:
+    """The (n_u, n_v, 3) float64 vertex grid of torus_knot_triangles' tube (u along the knot, v around it)."""
     u = np.arange(n_u, dtype=np.float64) * (2.0 * np.pi / n_u)
     v = np.arange(n_v, dtype=np.float64) * (2.0 * np.pi / n_v)
 
@@ -291,13 +314,49 @@ def torus_knot_triangles(n_u: int = 512, n_v: int = 256, p: int = 2, q: int = 3)
     n1 /= np.linalg.norm(n1, axis=-1, keepdims=True)
     n2 = np.cross(tang, n1)
     rad = 2.4
-    pts = (c[:, None, :] + rad * (np.cos(v)[None, :, None] * n1[:, None, :] + np.sin(v)[None, :, None] * n2[:, None, :]))
+    return c[:, None, :] + rad * (np.cos(v)[None, :, None] * n1[:, None, :] + np.sin(v)[None, :, None] * n2[:, None, :])
+
+
+def torus_knot_triangles(n_u: int = 512, n_v: int = 256, p: int = 2, q: int = 3) -> np.ndarray:
+    """A closed surface mesh for the global-scene path (the Airplane OBJ is absent): a (p, q) torus-knot tube,
+    2 * n_u * n_v triangles, centred at (0, 9, 0) in the Rubik's extent (~18 units across) so the model camera
+    and lights of src/main.cpp frame it.  Deterministic (float64 numpy, rounded once to float32)."""
+    pts = torus_knot_grid(n_u, n_v, p, q)
     i0 = np.arange(n_u)[:, None]
     j0 = np.arange(n_v)[None, :]
     i1, j1 = (i0 + 1) % n_u, (j0 + 1) % n_v
     a, b, cc, d = pts[i0, j0], pts[i1, j0], pts[i1, j1], pts[i0, j1]
     tri = np.stack([np.stack([a, b, cc], axis=-2), np.stack([a, cc, d], axis=-2)], axis=2)  # (n_u, n_v, 2, 3, 3)
     return tri.reshape(-1, 9).astype(np.float32)
+
+
+def write_textured_torus_knot_obj(path: str | pathlib.Path, mtllib: str, materials, n_u: int = 512, n_v: int = 256,
+                                  s_repeat: float = 3.0) -> pathlib.Path:
+    """The torus-knot tube as an OBJ with texture coordinates and several materials: `materials` (usemtl
+    names of the .mtl `mtllib`, which lies next to `path` with its textures) take equal consecutive
+    segments along the knot, and vertex (i, j) of the grid carries vt (s_repeat * i / n_u, j / n_v) --
+    the texture repeats s_repeat times along the knot (GL_REPEAT) and once around the tube.  Loaded with
+    SRT_LOAD_TEXCOORDS (the loader with has_texcoords set) every hit samples its material's texture at its
+    interpolated uv.  Positions are the float32 grid written with 9 significant digits (exact round trip)."""
+    path = pathlib.Path(path)
+    pts = torus_knot_grid(n_u, n_v).astype(np.float32).reshape(-1, 3)
+    i, j = np.meshgrid(np.arange(n_u), np.arange(n_v), indexing="ij")
+    st = np.stack([np.float32(s_repeat) * i.astype(np.float32) / np.float32(n_u),
+                   j.astype(np.float32) / np.float32(n_v)], axis=-1).reshape(-1, 2)
+    lines = [f"mtllib {mtllib}"]
+    lines += [f"v {x:.9g} {y:.9g} {z:.9g}" for x, y, z in pts.tolist()]
+    lines += [f"vt {a:.9g} {b:.9g}" for a, b in st.tolist()]
+    idx = lambda a, b: (a % n_u) * n_v + (b % n_v) + 1  # noqa: E731  (1-based, vertex and vt alike)
+    nm = len(materials)
+    for seg, m in enumerate(materials):
+        lines.append(f"usemtl {m}")
+        for a in range(seg * n_u // nm, (seg + 1) * n_u // nm):
+            for b in range(n_v):
+                A, B, C, D = idx(a, b), idx(a + 1, b), idx(a + 1, b + 1), idx(a, b + 1)
+                lines.append(f"f {A}/{A} {B}/{B} {C}/{C}")
+                lines.append(f"f {A}/{A} {C}/{C} {D}/{D}")
+    path.write_text("\n".join(lines) + "\n")
+    return path
 
 
 def torus_knot_model(n_u: int = 512, n_v: int = 256) -> Model:

@@ -17,8 +17,13 @@ Configs (BASELINE.json "configs"):
                                                                8-way band split reassembled
   C5 synthetic 10 M triangles 4096x4096 (512 spp in the config) -- full frame at the bench's 16 spp,
                                                                oracle rows, determinism
+  C5 at its configured 512 spp                               -- full frame, counting vs timed IL instance,
+                                                               oracle rows at 512 spp
   C3 stand-in: torus-knot surface mesh 1920x1080 @ 256 spp      -- C3's regime (global-scene mode, real
                                                                surface mesh) at C3's size, oracle rows
+  C3 stand-in with the Airplane's material set               -- the same surface carrying the Airplane's six
+                                                               .mtl materials and PNG textures, sampled at
+                                                               real uvs (the TEX instance), 1080p @ 256 spp
 Every render goes through the counting instance and then the timed instance the benchmark measures at
 that size, which must agree bit for bit.
 """
@@ -167,6 +172,61 @@ def test_c5_synthetic_10M_rows_and_determinism(c5_setup):
     assert_rows(a, o, acc, out, rows)
     b, p, _ = gpu_render(setup, spp, count=False)
     assert bits_equal(a, b).all() and (o == p).all()
+
+
+def test_c5_synthetic_10M_512spp_full_config(c5_setup):
+    """C5 as BASELINE.json configures it: 4096x4096 @ 512 spp on the 10 M-triangle scene.  The counting
+    instance and the timed IL instance agree bit for bit over the whole frame (both run every one of the
+    512 frames, in 16-GiB sample-buffer chunks), and the oracle renders three rows at 512 spp."""
+    setup = c5_setup
+    spp = 512
+    a, o, st = gpu_render(setup, spp)
+    assert st["samples"] == 4096 * 4096 * spp and st["stack_overflow"] == 0 and st["bounce_cap"] == 0
+    rows = spread_rows(4096, 3)
+    acc, out, _ = oracle_render(setup, spp, rows=rows)
+    assert_rows(a, o, acc, out, rows)
+    assert np.isfinite(a[..., :3]).all()
+
+
+AIRPLANE_MATERIALS = ("11803_Airplane_body", "11803_Airplane_wing_R", "11803_Airplane_wing_details_R",
+                      "11803_Airplane_tail", "11803_Airplane_wing_details_L", "11803_Airplane_wing_L")
+
+
+def test_c3_standin_airplane_materials_textured_1080p_256spp(tmp_path):
+    """C3's material path at C3's size (it ran only at 48x40): the 262,144-triangle surface
+    carries the Airplane's own six .mtl materials and 1024x1024 diffuse PNGs (tests/golden/objects, the
+    reference's assets), one segment of the knot each, with real per-vertex uvs (the loader with
+    has_texcoords set), so every hit samples its material's texture bilinearly at its interpolated uv
+    (TriangleToSupportedMat, raytrace_utils.glsl:140-175).  1920x1080 @ 256 spp through the timed texture
+    instance of global-scene mode (fused, 5 waves per SIMD), bit-equal to the counting instance over the
+    frame and to the oracle on rows spread across it."""
+    import shutil
+
+    src = OBJECTS / "11803_Airplane_v1_l1"
+    for f in src.iterdir():
+        shutil.copy(f, tmp_path / f.name)
+    obj = R.write_textured_torus_knot_obj(tmp_path / "knot_airplane.obj", "11803_Airplane_v1_l1.mtl",
+                                          AIRPLANE_MATERIALS)
+    model = S.load_obj(obj, texcoords=True)
+    assert model.info()["materials"] == 6 and model.info()["triangles"] == 262144
+    setup = R.make_setup(1920, 1080, show_model=True, models=[model])
+    sc = setup.scene
+    assert sc.sample_textures and (sc.mats["use_texture"] == 1).all() and len(sc.textures) == 6
+    assert float(sc.verts["uv"].max()) > 1.0  # uvs past 1: GL_REPEAT wrapping is exercised
+    assert timed_instance(setup) == "fused5"
+    spp = 256
+    a, o, st = gpu_render(setup, spp)
+    assert st["samples"] == 1920 * 1080 * spp and st["stack_overflow"] == 0
+    assert st["mat_reads"] > 0
+    rows = spread_rows(1080, 12)
+    acc, out, _ = oracle_render(setup, spp, rows=rows)
+    assert_rows(a, o, acc, out, rows)
+    # the textures matter: the constant-albedo (uv = (0,0)) load of the same OBJ renders a different frame
+    const = R.make_setup(1920, 1080, show_model=True, models=[S.load_obj(obj)])
+    assert not const.scene.sample_textures
+    ca, _, _ = oracle_render(const, 4, rows=rows[:2])
+    ta, _, _ = oracle_render(setup, 4, rows=rows[:2])
+    assert not bits_equal(ca[rows[:2]], ta[rows[:2]]).all()
 
 
 def test_c3_standin_surface_mesh_1080p_256spp():

@@ -678,11 +678,14 @@ def test_pipelined_launches_match_one_stream(rubik, monkeypatch, scene):
         monkeypatch.setenv("SRT_FORCE_GLOBAL_SCENE", "1")
     setup = (R.make_setup(56, 40, show_model=False, max_depth=4) if scene == "spheres"
              else R.make_setup(56, 40, show_model=True, models=[rubik]))
-    monkeypatch.setenv("SRT_SAMPLE_BUFFER_KB", str(56 * 40 * 16 * 3 // 1024 + 1))  # 3 frames per chunk
     got = {}
     for pipe, overlap in (("1", "1"), ("3", "2"), ("2", "2"), ("3", "1")):  # 1: overlap only for nranks > 1
         monkeypatch.setenv("SRT_PIPELINE", pipe)
         monkeypatch.setenv("SRT_PIPELINE_OVERLAP", overlap)
+        # 3 frames per chunk: SRT_SAMPLE_BUFFER_* is the context's whole budget, split over its own sample
+        # buffer and one per pipeline slot
+        nbuf = int(pipe) + 1 if int(pipe) > 1 else 1
+        monkeypatch.setenv("SRT_SAMPLE_BUFFER_KB", str(56 * 40 * 16 * 3 * nbuf // 1024 + 1))
         r = R.Renderer(setup)
         try:
             r.compute.kernel_time()
@@ -691,6 +694,8 @@ def test_pipelined_launches_match_one_stream(rubik, monkeypatch, scene):
             r.finish()
             ms, launches = r.compute.kernel_time()
             assert launches == 3 * 6 and ms > 0.0  # 16 frames in chunks of 3: 6 launches per render
+            assert r.compute.GetInt("launch.chunks") == 6
+            assert r.compute.GetInt("launch.overlap") == (1 if pipe != "1" and overlap == "2" else 0)
             got[pipe + "/" + overlap] = (r.accum(), r.output())
         finally:
             r.close()
