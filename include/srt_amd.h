@@ -122,21 +122,20 @@ int srt_finish(srt_context* ctx);
  * uniform at frame_first + nframes - 1, as the last dispatch would. */
 int srt_render_frames(srt_context* ctx, int frame_first, int nframes, int write_output, int count);
 int srt_get_stats(srt_context* ctx, srt_stats* out);
-/* Device time of the path-tracing kernel launches of the last render call,
- * from each sample_kernel / sphere_kernel launch's span (its first wave's start
- * to its last wave's end on the GPU's 100 MHz real-time clock): a launch counts
- * from its start, or from the end of the context's launch before it when that
- * is later, to its end -- its span when launches run in series, the interval
- * between consecutive launch ends when overlapped pipeline slots start it while
- * its predecessor drains (HIP events or rocprofv3's dispatch-to-end time would
- * also count its wait for the CUs).  HIP events around pool and wavefront
- * launches.  Waits for the render. */
+/* Device time of the path-tracing kernel launches of the last render call: the
+ * union of each sample_kernel / sphere_kernel launch's span (its first wave's
+ * start to its last wave's end on the GPU's 100 MHz real-time clock), plus HIP
+ * events around pool and wavefront launches.  Waits for the render.  Overlapped
+ * pipeline slots (SRT_PIPELINE_OVERLAP) dispatch a launch while others run, so
+ * its span may include time it shared the CUs with them. */
 int srt_last_kernel_ms(srt_context* ctx, float* ms);
-/* The same throughput time summed over every sample_kernel / sphere_kernel
- * launch since the previous call, and how many: a timed loop of renders
- * enqueued without synchronising reads its kernel time once.  Waits for them.
- * SRT_ERR_LIMIT when more than 4096 launches went unread (their records are
- * overwritten): the total would cover only part of them. */
+/* The device time of every sample_kernel / sphere_kernel launch since the
+ * previous call -- the union of their spans, the time during which some launch
+ * of the context ran (launches in series add their spans; overlapped ones, which
+ * the hardware may also run side by side, count their shared time once) -- and
+ * how many: a timed loop of renders enqueued without synchronising reads its
+ * kernel time once.  Waits for them.  SRT_ERR_LIMIT when more than 4096 launches
+ * went unread (their records are overwritten). */
 int srt_kernel_time(srt_context* ctx, double* total_ms, int* launches);
 int srt_reset_stats(srt_context* ctx);  /* also zeroes the NaN counter */
 /* Failure detection: path samples with a NaN component accumulated since the

@@ -83,6 +83,10 @@ enum { ST_RAYS = 0, ST_NODES, ST_TRIS, ST_RNGU, ST_RNGSQ, ST_LIGHTS, ST_MATS, ST
        // per traversal sub-step k < 16: lanes taking it (summed), waves executing it, lanes popping after it
        ST_DBG_SUB, ST_POOLERR = ST_DBG_SUB + 48,  // pool_kernel's watchdog fired (pool.hpp)
        ST_TOTAL };
+// SRT_PHASE_TIMING builds, in the last two sub-steps' slots (no pattern has 15 sub-steps): traversing lanes
+// summed per traversal iteration by ray kind (shadow, camera, bounce), and ray starts by kind (camera,
+// shadow, bounce)
+constexpr int ST_DBG_KIND = ST_DBG_SUB + 42;
 
 // Diagnostic build only (-DSRT_SUBSTEP_STATS): per-sub-step lane counts (global atomics, slow).
 #ifdef SRT_SUBSTEP_STATS

@@ -324,7 +324,13 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
   tr.start = false;
   tr.hit = kNoneRef;
 
+#ifdef SRT_PHASE_TIMING
+  unsigned long long d_kind[6] = {0, 0, 0, 0, 0, 0};  // (ST_DBG_KIND)
+#endif
   auto start_ray = [&]() {
+#ifdef SRT_PHASE_TIMING
+    d_kind[shadow_phase ? 4 : (bounces == 0 ? 3 : 5)] += 1;  // per lane (ray starts by kind)
+#endif
     tr.dist = tmax;
     tr.hit = kNoneRef;
     tr.bi = 0;
@@ -482,6 +488,9 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
         ++d_titers;
         d_work += __popcll(__ballot(has_work));
         d_trav += __popcll(trav);
+        d_kind[0] += __popcll(__ballot(tr.active && shadow_phase));
+        d_kind[1] += __popcll(__ballot(tr.active && !shadow_phase && bounces == 0));
+        d_kind[2] += __popcll(__ballot(tr.active && !shadow_phase && bounces > 0));
         d_leaf += __popcll(__ballot(tr.active && trav_at_leaf(tr.cnt)));
         d_int += __popcll(__ballot(tr.active && tr.cnt == 0));
 #endif
@@ -565,6 +574,14 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
     atomicAdd(&kp.stats[ST_DBG_LEAF], d_leaf);
     atomicAdd(&kp.stats[ST_DBG_INT], d_int);
     atomicAdd(&kp.stats[ST_DBG_SHADE], d_shade);
+    for (int k = 0; k < 3; ++k) atomicAdd(&kp.stats[ST_DBG_KIND + k], d_kind[k]);
+  }
+  {  // ray starts were counted per lane
+    for (int k = 3; k < 6; ++k) {
+      unsigned long long v = d_kind[k];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if (lane == 0) atomicAdd(&kp.stats[ST_DBG_KIND + k], v);
+    }
   }
 #endif
 #ifdef SRT_WAVE_TRACE

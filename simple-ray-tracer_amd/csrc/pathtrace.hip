@@ -217,10 +217,9 @@ struct srt_context {
   int pipe = 3;                    // SRT_PIPELINE
   // SRT_PIPELINE_OVERLAP: whether a sample launch may start before the previous one ends (2, the default:
   // always; 1: on a rank's share of a multi-GPU split (nranks > 1) only; 0: never).  An overlapped launch's
-  // dispatch-to-end time (rocprofv3) and span include its wait for the CUs its predecessor still holds, so
-  // kernel time is a throughput time: each launch counts from its start or its predecessor's end, whichever
-  // is later, to its end (srt_kernel_time; tools/trace_intervals.py applies the same rule to rocprofv3's
-  // kernel trace).
+  // dispatch-to-end time (rocprofv3) and span include its wait for the CUs other launches hold, so kernel
+  // time is the union of the launches' spans (srt_kernel_time; tools/trace_intervals.py takes the same
+  // union over rocprofv3's kernel trace).
   int pipe_overlap = 2;
   hipEvent_t last_sampled = nullptr;  // the last sample launch's end (a slot's `sampled`, or plain_done)
   hipEvent_t plain_done = nullptr;    // recorded on `stream` after a launch outside the slots
@@ -232,6 +231,7 @@ struct srt_context {
   unsigned long long* d_span = nullptr;
   static constexpr int kSpanCap = 4096;
   unsigned long long span_seq = 0, span_read = 0;  // records written / summed by srt_kernel_time
+  unsigned long long span_done = 0;                 // the latest end srt_kernel_time has counted (a tick)
   std::vector<long long> chunk_span;               // per chunk of the last render: its record (or -1)
   hipEvent_t lidle = nullptr;      // synchronized before the current launch frees a launch buffer
   hipEvent_t lidle2 = nullptr;     // (and this: the previous launch, for the buffers launches in series share)
@@ -1559,11 +1559,11 @@ extern "C" int srt_debug_wave_trace(srt_context* c, unsigned long long* out, int
 #endif
 
 // Kernel time of sample launches from their span records (first wave's start, last wave's end; 100 MHz
-// ticks).  Launch q counts from its start, or from the end of launch q - 1 (the context's launch before it)
-// when that is later, to its end: its own span when launches run in series, the interval between
-// consecutive launch ends when a launch is dispatched while its predecessor drains (overlapped pipeline
-// slots, whose spans include the wait for the CUs the predecessor still holds).  The sum over launches is
-// the time during which some sample launch of the context runs.
+// ticks): the time during which some sample launch of the context runs, i.e. the union of the spans.
+// Launches in series add their spans.  Overlapped pipeline slots dispatch a launch while its
+// predecessor still runs -- it starts in the CUs the drain frees, or, when the host has enqueued several
+// ahead, the hardware may run two slots' launches side by side or the later one first -- so a span then
+// includes the wait for CUs another launch holds, and only the union is the launches' device time.
 namespace {
 bool SpanRecord(const srt_context* c, const unsigned long long* ring, unsigned long long q, unsigned long long* t0,
                 unsigned long long* t1) {
@@ -1574,11 +1574,24 @@ bool SpanRecord(const srt_context* c, const unsigned long long* ring, unsigned l
   *t1 = sp[1];
   return true;
 }
-double SpanCreditMs(const srt_context* c, const unsigned long long* ring, unsigned long long q) {
-  unsigned long long t0, t1, p0, p1;
-  if (!SpanRecord(c, ring, q, &t0, &t1)) return 0.0;
-  if (q > 0 && SpanRecord(c, ring, q - 1, &p0, &p1) && p1 > t0) t0 = std::min(p1, t1);
-  return (double)(t1 - t0) * 1e-5;
+// Union of the spans of records [from, to) in ms, counting only time after `after` (a tick); *last_end
+// receives the latest end seen (or `after`).
+double SpanUnionMs(const srt_context* c, const unsigned long long* ring, unsigned long long from,
+                   unsigned long long to, unsigned long long after, unsigned long long* last_end) {
+  std::vector<std::pair<unsigned long long, unsigned long long>> iv;
+  for (unsigned long long q = from; q < to; ++q) {
+    unsigned long long t0, t1;
+    if (SpanRecord(c, ring, q, &t0, &t1)) iv.push_back({std::max(t0, after), std::max(t1, after)});
+  }
+  std::sort(iv.begin(), iv.end());
+  unsigned long long covered = 0, reach = after;
+  for (const auto& [a, b] : iv) {
+    const unsigned long long lo = std::max(a, reach);
+    if (b > lo) covered += b - lo;
+    reach = std::max(reach, b);
+  }
+  if (last_end) *last_end = reach;
+  return (double)covered * 1e-5;
 }
 }  // namespace
 
@@ -1586,22 +1599,24 @@ int srt_last_kernel_ms(srt_context* c, float* ms) {
   if (!c || !ms) return SRT_ERR_INVALID;
   *ms = 0.0f;
   std::vector<unsigned long long> ring;
+  unsigned long long lo = ~0ull, hi = 0;  // the render's span records (its chunks' launches are consecutive)
   for (int i = 0; i + 1 < c->ev_used; i += 2) {
     HIP_OK(hipEventSynchronize(c->ev[i + 1]));
     const size_t chunk = (size_t)(i / 2);
     const long long rec = chunk < c->chunk_span.size() ? c->chunk_span[chunk] : -1;
     if (rec >= 0 && (unsigned long long)rec + srt_context::kSpanCap >= c->span_seq) {  // the launch's own span
-      if (ring.empty()) {
-        if (int rq = Quiesce(c)) return rq;  // (the launch before the render's first may be another slot's)
-        ring.resize(2 * srt_context::kSpanCap);
-        HIP_OK(hipMemcpy(ring.data(), c->d_span, sizeof(unsigned long long) * ring.size(), hipMemcpyDeviceToHost));
-      }
-      *ms += (float)SpanCreditMs(c, ring.data(), (unsigned long long)rec);
+      lo = std::min(lo, (unsigned long long)rec);
+      hi = std::max(hi, (unsigned long long)rec + 1);
       continue;
     }
     float t = 0.0f;  // pool and wavefront launches: the HIP events around them
     HIP_OK(hipEventElapsedTime(&t, c->ev[i], c->ev[i + 1]));
     *ms += t;
+  }
+  if (lo < hi) {
+    ring.resize(2 * srt_context::kSpanCap);
+    HIP_OK(hipMemcpy(ring.data(), c->d_span, sizeof(unsigned long long) * ring.size(), hipMemcpyDeviceToHost));
+    *ms += (float)SpanUnionMs(c, ring.data(), lo, hi, 0ull, nullptr);
   }
   return SRT_OK;
 }
@@ -1621,10 +1636,9 @@ int srt_kernel_time(srt_context* c, double* total_ms, int* launches) {
   if (c->span_seq > from) {
     std::vector<unsigned long long> ring(2 * srt_context::kSpanCap);
     HIP_OK(hipMemcpy(ring.data(), c->d_span, sizeof(unsigned long long) * ring.size(), hipMemcpyDeviceToHost));
-    for (unsigned long long q = from; q < c->span_seq; ++q) {
-      *total_ms += SpanCreditMs(c, ring.data(), q);
-      ++*launches;
-    }
+    // (time before the end of the launches read by the previous call was counted there)
+    *total_ms = SpanUnionMs(c, ring.data(), from, c->span_seq, c->span_done, &c->span_done);
+    *launches = (int)(c->span_seq - from);
   }
   return SRT_OK;
 }

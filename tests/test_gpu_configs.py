@@ -224,9 +224,9 @@ def test_c3_standin_airplane_materials_textured_1080p_256spp(tmp_path):
     # the textures matter: the constant-albedo (uv = (0,0)) load of the same OBJ renders a different frame
     const = R.make_setup(1920, 1080, show_model=True, models=[S.load_obj(obj)])
     assert not const.scene.sample_textures
-    ca, _, _ = oracle_render(const, 4, rows=rows[:2])
-    ta, _, _ = oracle_render(setup, 4, rows=rows[:2])
-    assert not bits_equal(ca[rows[:2]], ta[rows[:2]]).all()
+    ca, _, _ = oracle_render(const, 2, rows=rows)
+    ta, _, _ = oracle_render(setup, 2, rows=rows)
+    assert not bits_equal(ca[rows], ta[rows]).all()
 
 
 def test_c3_standin_surface_mesh_1080p_256spp():

@@ -7,6 +7,10 @@ the timed launch's kernel time and its counters, per launch.
   lane_util       SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU)
   wait_any        SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked on s_waitcnt)
   wait_inst       SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (issue stalls)
+  valu_busy       cycle-weighted: 4 x SQ_ACTIVE_INST_VALU (quad-cycles waves spend executing VALU instructions)
+                  / (1024 SIMDs x the pass's cycles, GRBM_GUI_ACTIVE / 8 XCDs): a slow instruction weighs its cycles
+  valu2_share     SQ_ACTIVE_INST_VALU2 / SQ_ACTIVE_INST_VALU (quad-cycles in which two VALU instructions issue)
+  cycles_per_valu 4 x SQ_ACTIVE_INST_VALU / SQ_INSTS_VALU (2 for a plain wave64 instruction)
   l2_hit          TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
   fetch_lines_B   2 x FETCH_SIZE (128-B line requests tallied at 64 B on gfx950), per launch and per sample
   write_B         WRITE_SIZE, per launch and per sample (a sample's record is 16 B)
@@ -27,7 +31,7 @@ KERNEL = "void srt::sphere_kernel<false>"
 
 def counters(d: pathlib.Path, kernel: str = KERNEL) -> dict:
     out = {}
-    for sub in ("pmc_sq", "pmc_sq2", "pmc_fetch", "pmc_write", "pmc_tcc", "pmc_tcp"):
+    for sub in ("pmc_sq", "pmc_sq2", "pmc_cyc", "pmc_fetch", "pmc_write", "pmc_tcc", "pmc_tcp"):
         p = d / sub / "run_counter_collection.csv"
         if not p.exists():
             continue
@@ -64,6 +68,15 @@ def main():
             e["valu_issue"] = c["SQ_INSTS_VALU"] * 2 / (SIMDS * ks * CLOCK)
             e["lane_util"] = c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_INSTS_VALU"])
             e["wait_any"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
+        if "SQ_ACTIVE_INST_VALU" in c and "GRBM_GUI_ACTIVE" in c:
+            cyc = c["GRBM_GUI_ACTIVE"] / 8.0  # (the pass's own cycles; summed over the 8 XCDs)
+            e["valu_busy"] = 4.0 * c["SQ_ACTIVE_INST_VALU"] / (SIMDS * cyc)
+            e["valu2_share"] = c.get("SQ_ACTIVE_INST_VALU2", 0.0) / max(c["SQ_ACTIVE_INST_VALU"], 1.0)
+            e["sca_busy"] = 4.0 * c.get("SQ_ACTIVE_INST_SCA", 0.0) / (SIMDS * cyc)
+            if "SQ_INSTS_VALU" in c:
+                e["cycles_per_valu"] = 4.0 * c["SQ_ACTIVE_INST_VALU"] / c["SQ_INSTS_VALU"]
+                e["trans_share"] = c.get("SQ_INSTS_VALU_TRANS_F32", 0.0) / c["SQ_INSTS_VALU"]
+                e["f64_share"] = (c.get("SQ_INSTS_VALU_MUL_F64", 0.0) + c.get("SQ_INSTS_VALU_FMA_F64", 0.0)) / c["SQ_INSTS_VALU"]
         if "SQ_WAIT_INST_ANY" in c and "SQ_WAVE_CYCLES" in c:
             e["wait_inst"] = c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"]
             e["active_inst"] = c["SQ_ACTIVE_INST_ANY"] / c["SQ_WAVE_CYCLES"] if "SQ_ACTIVE_INST_ANY" in c else None
@@ -82,7 +95,8 @@ def main():
             e["write_B_per_sample"] = e["write_B"] / samples
         res["by_blocks"][str(n)] = e
     outp.write_text(json.dumps(res, indent=1) + "\n")
-    keys = ("kernel_ms", "valu_issue", "lane_util", "wait_any", "wait_inst", "active_inst", "l2_hit",
+    keys = ("kernel_ms", "valu_issue", "valu_busy", "cycles_per_valu", "valu2_share", "sca_busy", "trans_share",
+            "f64_share", "lane_util", "wait_any", "wait_inst", "active_inst", "l2_hit",
             "l1_miss_req_frac", "fetch_lines_B_per_sample", "write_B_per_sample", "sq_insts_valu_per_ray",
             "sq_insts_salu_per_ray", "sq_insts_vmem_rd_per_ray", "sq_insts_lds_per_ray")
     print("blocks " + " ".join(keys))

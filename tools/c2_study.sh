@@ -14,6 +14,12 @@ for n in ${BLOCKS:-3 4 5 6}; do
     SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_SALU --output-format csv -d $O/pmc_sq -o run -- $B > $O/pmc_sq.log 2>&1 || exit 1
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE \
     --output-format csv -d $O/pmc_sq2 -o run -- $B > $O/pmc_sq2.log 2>&1 || exit 1
+  # cycle-weighted VALU: the quad-cycles waves spend executing VALU instructions (a slow instruction -- the f64
+  # multiplies of pow(x, 5), v_rcp/v_sqrt/v_sin, the v_div_* sequences -- weighs its cycles, not 1)
+  timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_ACTIVE_INST_SCA SQ_INSTS_VALU_TRANS_F32 \
+    SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --output-format csv \
+    -d $O/pmc_cyc -o run -- $B > $O/pmc_cyc.log 2>&1 || exit 1
+  [ -n "$CYC_ONLY" ] && { echo "b$n cyc done"; continue; }
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- $B > $O/pmc_fetch.log 2>&1 || exit 1
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- $B > $O/pmc_write.log 2>&1 || exit 1
   timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $O/pmc_tcc -o run -- $B > $O/pmc_tcc.log 2>&1 || exit 1

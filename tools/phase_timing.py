@@ -6,7 +6,9 @@ sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd")); sys.path.insert(0, str(
 import srt_amd as S
 from srt_amd import render as R, _lib
 spp = int(sys.argv[1]) if len(sys.argv) > 1 else 32
-setup = R.make_setup(1920, 1080, show_model=True, models=[R.rubik_model(ROOT / "tests/golden/objects")])
+scene = sys.argv[2] if len(sys.argv) > 2 else "rubik"
+model = R.torus_knot_model() if scene == "torusknot" else R.rubik_model(ROOT / "tests/golden/objects")
+setup = R.make_setup(1920, 1080, show_model=True, models=[model])
 r = R.Renderer(setup)
 r.render(spp); r.finish()
 r.render(spp); r.finish()
@@ -25,3 +27,10 @@ for k in range(16):
     if waves:
         print("  sub-step %2d: executed in %5.1f%% of iterations, %4.1f lanes when executed, %4.1f lanes pop after it"
               % (k, 100 * waves / ti, lanes / waves, pops / ti))
+# ray kinds (ST_DBG_KIND, in sub-steps 14-15's slots): traversing lanes summed per traversal iteration by the kind
+# of their ray, and ray starts by kind -- how much of the traversal a shadow ray and its bounce ray could share
+kt = [float(v) for v in out[52:55]]
+ks = [float(v) for v in out[55:58]]
+if sum(kt):
+    print("traversal lane-iterations: shadow %.1f%% camera %.1f%% bounce %.1f%%; ray starts: camera %.0f shadow %.0f "
+          "bounce %.0f" % (100 * kt[0] / sum(kt), 100 * kt[1] / sum(kt), 100 * kt[2] / sum(kt), ks[0], ks[1], ks[2]))

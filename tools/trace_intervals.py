@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """Throughput time per launch of a kernel from a rocprofv3 kernel trace: the check of bench.py's kernel_ms.
 
-Overlapped sample launches (pipeline slots) are dispatched while the previous launch
-still holds the CUs, so a dispatch's Start..End includes its wait for them.  The rule bench.py reads from
-the launches' own spans (srt_kernel_time) is applied here to the trace's timestamps: launch k counts from
-max(Start_k, End_{k-1}) to End_k -- the interval between consecutive launch ends when launches overlap, the
-dispatch's duration when they run in series.
+Overlapped sample launches (pipeline slots) are dispatched while other launches
+still hold the CUs (the hardware may also run two slots' launches side by side, or the later one first),
+so a dispatch's Start..End includes its wait for them.  bench.py's kernel time is the union of the
+launches' own spans (srt_kernel_time); here the same union is taken over the trace's timestamps: in start
+order, launch k adds the part of [Start_k, End_k] after the latest end so far -- the interval between
+consecutive launch ends when launches overlap, the dispatch's duration when they run in series.
 
   python tools/trace_intervals.py <run_kernel_trace.csv> <kernel-name substring> [last N] [bench line json]
 
@@ -21,7 +22,7 @@ import sys
 
 
 def throughput_ms(rows) -> list[float]:
-    """Per launch, in dispatch order: End_k - max(Start_k, End_{k-1}) in ms (the first: its own duration)."""
+    """Per launch, in start order: what it adds to the union of the dispatches' intervals, in ms."""
     out, prev_end = [], None
     for r in rows:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
