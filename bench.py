@@ -76,7 +76,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default="rubik", choices=("rubik", "spheres", "synthetic", "torusknot"))
+    ap.add_argument("--scene", default="rubik", choices=("rubik", "spheres", "synthetic", "torusknot", "airplane_knot"))
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=256)
@@ -90,6 +90,8 @@ def parse(argv=None):
     ap.add_argument("--global-spp", type=int, default=16)
     ap.add_argument("--no-surface-leg", action="store_true", help="skip the 262k-triangle surface-mesh leg")
     ap.add_argument("--surface-spp", type=int, default=64)
+    ap.add_argument("--no-airplane-leg", action="store_true",
+                    help="skip the surface mesh carrying the Airplane's textured materials (C3's material path)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (multi-rank tests on one GPU)")
     ap.add_argument("--group", action="store_true",
@@ -207,6 +209,7 @@ def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str, globa
         "valu_lane_utilisation": round(cnt["SQ_THREAD_CYCLES_VALU"] / (64.0 * cnt["SQ_INSTS_VALU"]), 4),
         "useful_valu_frac": round(fr["valu_issue"] * cnt["SQ_THREAD_CYCLES_VALU"] / (64.0 * cnt["SQ_INSTS_VALU"]), 4),
         "lds_bank_conflict_frac": round(cnt["SQ_LDS_BANK_CONFLICT"] / max(cnt["SQ_LDS_IDX_ACTIVE"], 1.0), 4),
+        **issue_split(cnt, k_s),
         "counters_source": cnt.get("source", ""),
         "counters_code_hash": cnt.get("code_hash"),
         "note": "frac = the bound roof's fraction at the live kernel time; per-launch counters from the committed "
@@ -222,6 +225,25 @@ def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str, globa
     return r
 
 
+def issue_split(cnt: dict, k_s: float) -> dict:
+    """Where a wave's cycles go, from the second SQ pass (tools/profile_round.sh): issuing an instruction
+    (SQ_ACTIVE_INST_ANY: one quad-cycle per instruction), waiting on memory / LDS (SQ_WAIT_ANY) or stalled on
+    issue (SQ_WAIT_INST_ANY), as fractions of SQ_WAVE_CYCLES (they sum to ~1); instructions issued per SIMD
+    per quad-cycle (each wave issues at most one); the share of VALU quad-cycles that issued two VALU
+    instructions (SQ_ACTIVE_INST_VALU2, from two waves)."""
+    if "SQ_ACTIVE_INST_ANY" not in cnt or "SQ_WAVE_CYCLES" not in cnt:
+        return {}
+    w = cnt["SQ_WAVE_CYCLES"]
+    out = {"wave_cycles": {"issuing": round(cnt["SQ_ACTIVE_INST_ANY"] / w, 4),
+                           "waiting": round(cnt["SQ_WAIT_ANY"] / w, 4),
+                           "issue_stalled": round(cnt.get("SQ_WAIT_INST_ANY", float("nan")) / w, 4)},
+           "instructions_per_simd_quad_cycle": round(cnt["SQ_ACTIVE_INST_ANY"] / (SIMDS * k_s * CLOCK_HZ / 4), 4)}
+    if "SQ_ACTIVE_INST_VALU2" in cnt and "SQ_ACTIVE_INST_VALU" in cnt:
+        v, v2 = cnt["SQ_ACTIVE_INST_VALU"], cnt["SQ_ACTIVE_INST_VALU2"]
+        out["valu_dual_issue_share"] = round(v2 / max(v - v2, 1.0), 4)
+    return out
+
+
 def build_setup(scene: str, W: int, H: int, spp: int, max_depth: int, synthetic_tris: int):
     from srt_amd import render as R
 
@@ -234,11 +256,38 @@ def build_setup(scene: str, W: int, H: int, spp: int, max_depth: int, synthetic_
     elif scene == "torusknot":
         models = [R.torus_knot_model()]
         show_model, wl = True, f"torusknot262144_{W}x{H}_{spp}spp"
+    elif scene == "airplane_knot":
+        models = [airplane_knot_model()]
+        show_model, wl = True, f"torusknot262144_airplane_materials_{W}x{H}_{spp}spp"
     else:
         models, show_model, wl = None, False, f"spheres_{W}x{H}_{spp}spp"
     if max_depth != 5:
         wl += f"_depth{max_depth}"
     return R.make_setup(W, H, show_model=show_model, models=models, max_depth=max_depth), wl
+
+
+AIRPLANE_MATERIALS = ("11803_Airplane_body", "11803_Airplane_wing_R", "11803_Airplane_wing_details_R",
+                      "11803_Airplane_tail", "11803_Airplane_wing_details_L", "11803_Airplane_wing_L")
+
+
+def airplane_knot_model():
+    """C3's material path on the surface mesh: the torus-knot tube (outward faces) carrying the Airplane's six
+    .mtl materials and 1024x1024 diffuse PNGs (the reference's assets, tests/golden/objects), one segment each,
+    with real per-vertex uvs loaded (has_texcoords set): every hit samples its texture at its uv
+    (srt_amd.render.write_textured_torus_knot_obj; tests/test_gpu_configs.py renders it at 1080p @256 spp)."""
+    import shutil
+    import tempfile
+
+    import srt_amd as S
+    from srt_amd import render as R
+
+    src = ROOT / "tests" / "golden" / "objects" / "11803_Airplane_v1_l1"
+    with tempfile.TemporaryDirectory() as d:
+        d = pathlib.Path(d)
+        for f in src.iterdir():
+            shutil.copy(f, d / f.name)
+        obj = R.write_textured_torus_knot_obj(d / "knot_airplane.obj", "11803_Airplane_v1_l1.mtl", AIRPLANE_MATERIALS)
+        return S.load_obj(obj, texcoords=True)
 
 
 class RankRun:
@@ -488,16 +537,19 @@ KERNEL_LDS = "srt::sample_kernel<false, true, true, 1024, false, false, 4> (LDS-
 
 def timed_kernel(c, scene: str) -> str:
     """The sample_kernel instance the run's timed launches took.  Global-scene mode: fused sub-steps for
-    trees under 600 MB (both legs), the IL pattern past it (C5); the fused instance at 5 waves per SIMD
-    for trees under 48 MB (the surface-mesh leg), else 4 (srt_get_int's scene.* names)."""
+    trees under 600 MB (the legs), the IL pattern past it (C5); the fused instance at 5 waves per SIMD
+    for trees under 48 MB (the surface-mesh legs), else 4 (srt_get_int's scene.* names); the texture
+    instance when materials sample their textures (the Airplane-material leg)."""
     if scene == "rubik":
         return KERNEL_LDS
     if scene == "spheres":
         return "srt::sphere_kernel<false> (spheres: no BVH, 5 waves per SIMD)"
     fused = c.GetInt("scene.fused") == 1
     gw = c.GetInt("scene.global_waves") if fused else 4
-    return (f"srt::sample_kernel<false, false, true, 256, false, {'true' if fused else 'false'}, {gw}> "
-            f"(global-scene mode, {'fused' if fused else 'IL'} sub-steps, {gw} waves per SIMD)")
+    tex = scene == "airplane_knot"
+    return (f"srt::sample_kernel<false, false, true, 256, {'true' if tex else 'false'}, {'true' if fused else 'false'}, "
+            f"{gw}> (global-scene mode, {'fused' if fused else 'IL'} sub-steps, {gw} waves per SIMD"
+            f"{', textures sampled per hit' if tex else ''})")
 
 
 def run_compute(run):
@@ -557,12 +609,13 @@ def main(argv=None):
     par = parallelism(args, mode, world, run)
     table = rank_table(per_ctx, run.rank_stats() if mode == "group" else [st], args, mode, world, dev)
     run.close()
-    global_main = args.scene in ("synthetic", "torusknot")
+    global_main = args.scene in ("synthetic", "torusknot", "airplane_knot")
 
     legs = []
     for leg, enabled, scene, lw, lh, lspp, ntri in (
             ("global_scene", not args.no_global_leg, "synthetic", 1920, 1080, args.global_spp, args.global_tris),
-            ("surface_mesh", not args.no_surface_leg, "torusknot", 1920, 1080, args.surface_spp, 0)):
+            ("surface_mesh", not args.no_surface_leg, "torusknot", 1920, 1080, args.surface_spp, 0),
+            ("airplane_materials", not args.no_airplane_leg, "airplane_knot", 1920, 1080, args.surface_spp, 0)):
         if not enabled:
             continue
         lsetup, lname = build_setup(scene, lw, lh, lspp, 5, ntri)
@@ -574,7 +627,9 @@ def main(argv=None):
         if rank == 0:
             desc = (f"synthetic {ntri} triangles (SURVEY 8d generator)" if scene == "synthetic" else
                     "torus-knot tube, 262144 triangles (closed surface mesh; srt_amd.render.torus_knot_triangles), "
-                    "model camera and lights")
+                    "model camera and lights" if scene == "torusknot" else
+                    "the torus-knot tube with outward faces carrying the Airplane's six .mtl materials and diffuse "
+                    "PNGs, textures sampled at each hit's uv (C3's material path; bench.airplane_knot_model)")
             l_ranks = per_rank_lines(l_table, lname, l_kname, True)
             legs.append({
                 "leg": leg, "workload": lname, "value": round(l_rays * args.steps / l_el / 1e6, 3),

@@ -331,13 +331,17 @@ def torus_knot_triangles(n_u: int = 512, n_v: int = 256, p: int = 2, q: int = 3)
 
 
 def write_textured_torus_knot_obj(path: str | pathlib.Path, mtllib: str, materials, n_u: int = 512, n_v: int = 256,
-                                  s_repeat: float = 3.0) -> pathlib.Path:
+                                  s_repeat: float = 3.0, outward: bool = True) -> pathlib.Path:
     """The torus-knot tube as an OBJ with texture coordinates and several materials: `materials` (usemtl
     names of the .mtl `mtllib`, which lies next to `path` with its textures) take equal consecutive
     segments along the knot, and vertex (i, j) of the grid carries vt (s_repeat * i / n_u, j / n_v) --
     the texture repeats s_repeat times along the knot (GL_REPEAT) and once around the tube.  Loaded with
     SRT_LOAD_TEXCOORDS (the loader with has_texcoords set) every hit samples its material's texture at its
-    interpolated uv.  Positions are the float32 grid written with 9 significant digits (exact round trip)."""
+    interpolated uv.  Positions are the float32 grid written with 9 significant digits (exact round trip).
+    `outward`: faces wound so that the geometric normal (normalize(cross(e1, e2)), which the shader uses as
+    is, ray_intersects.glsl:95) points out of the tube, as an exported model's does -- paths then bounce off
+    the surface (SampleIndirectNew rejects dot(N, V) <= 0, brdf.glsl:239-277); torus_knot_triangles' winding
+    points inward, so its paths end at the first hit after the shadow ray."""
     path = pathlib.Path(path)
     pts = torus_knot_grid(n_u, n_v).astype(np.float32).reshape(-1, 3)
     i, j = np.meshgrid(np.arange(n_u), np.arange(n_v), indexing="ij")
@@ -353,8 +357,12 @@ def write_textured_torus_knot_obj(path: str | pathlib.Path, mtllib: str, materia
         for a in range(seg * n_u // nm, (seg + 1) * n_u // nm):
             for b in range(n_v):
                 A, B, C, D = idx(a, b), idx(a + 1, b), idx(a + 1, b + 1), idx(a, b + 1)
-                lines.append(f"f {A}/{A} {B}/{B} {C}/{C}")
-                lines.append(f"f {A}/{A} {C}/{C} {D}/{D}")
+                if outward:
+                    lines.append(f"f {A}/{A} {C}/{C} {B}/{B}")
+                    lines.append(f"f {A}/{A} {D}/{D} {C}/{C}")
+                else:
+                    lines.append(f"f {A}/{A} {B}/{B} {C}/{C}")
+                    lines.append(f"f {A}/{A} {C}/{C} {D}/{D}")
     path.write_text("\n".join(lines) + "\n")
     return path
 

@@ -197,7 +197,8 @@ def test_c3_standin_airplane_materials_textured_1080p_256spp(tmp_path):
     carries the Airplane's own six .mtl materials and 1024x1024 diffuse PNGs (tests/golden/objects, the
     reference's assets), one segment of the knot each, with real per-vertex uvs (the loader with
     has_texcoords set), so every hit samples its material's texture bilinearly at its interpolated uv
-    (TriangleToSupportedMat, raytrace_utils.glsl:140-175).  1920x1080 @ 256 spp through the timed texture
+    (TriangleToSupportedMat, raytrace_utils.glsl:140-175).  Its faces are wound outward, as an exported
+    model's are, so paths bounce off the surface and sample textures at their bounce hits too.  1920x1080 @ 256 spp through the timed texture
     instance of global-scene mode (fused, 5 waves per SIMD), bit-equal to the counting instance over the
     frame and to the oracle on rows spread across it."""
     import shutil
@@ -218,6 +219,9 @@ def test_c3_standin_airplane_materials_textured_1080p_256spp(tmp_path):
     a, o, st = gpu_render(setup, spp)
     assert st["samples"] == 1920 * 1080 * spp and st["stack_overflow"] == 0
     assert st["mat_reads"] > 0
+    # bounce rays: each shaded hit (one material read) traces a shadow ray and, off an outward face, mostly a
+    # bounce ray as well (inward faces end the path after the shadow ray: about one secondary ray per hit)
+    assert st["rays"] - st["samples"] > 1.3 * st["mat_reads"]
     rows = spread_rows(1080, 12)
     acc, out, _ = oracle_render(setup, spp, rows=rows)
     assert_rows(a, o, acc, out, rows)

@@ -241,7 +241,7 @@ def test_bench_in_process_group_same_device(tmp_path):
         dump = tmp_path / f"f{n}.npz"
         cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(n)[0], "--steps", "2", "--warmup", "1",
                "--width", str(W), "--height", str(H), "--spp", str(SPP), "--band-rows", "2", "--no-cpu-baseline",
-               "--no-global-leg", "--no-surface-leg", "--dump", str(dump)] + extra
+               "--no-global-leg", "--no-surface-leg", "--no-airplane-leg", "--dump", str(dump)] + extra
         env = {k: v for k, v in __import__("os").environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
         res = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=env)
         assert res.returncode == 0, res.stderr[-3000:]
@@ -278,7 +278,7 @@ def test_bench_group_of_one_agrees_with_single(tmp_path):
     vals = {}
     for name, extra in (("single", []), ("group", ["--group"]), ("single2", []), ("group2", ["--group"])):
         cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "1", "--steps", "6", "--warmup", "1",
-               "--no-cpu-baseline", "--no-global-leg", "--no-surface-leg"] + extra
+               "--no-cpu-baseline", "--no-global-leg", "--no-surface-leg", "--no-airplane-leg"] + extra
         res = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
         assert res.returncode == 0, res.stderr[-3000:]
         line = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])

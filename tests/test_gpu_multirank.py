@@ -46,7 +46,7 @@ def _run_bench(tmp_path: pathlib.Path, world: int, band: int):
     dump = tmp_path / f"frame_w{world}_b{band}.npz"
     cmd = [sys.executable, "-X", "faulthandler", str(ROOT / "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
            "--width", str(W), "--height", str(H), "--spp", str(SPP), "--band-rows", str(band),
-           "--no-cpu-baseline", "--no-global-leg", "--no-surface-leg", "--backend", "gloo", "--same-device", "--dump", str(dump)]
+           "--no-cpu-baseline", "--no-global-leg", "--no-surface-leg", "--no-airplane-leg", "--backend", "gloo", "--same-device", "--dump", str(dump)]
     procs = []
     for rank in range(world):
         env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),

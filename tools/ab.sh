@@ -10,7 +10,7 @@
 # Lines go to gpurun_out/$TAG/results.txt; the script stops at the first failing run.
 cd /root/repo && export TMPDIR=/tmp
 TAG=${TAG:-ab}; O=gpurun_out/$TAG; mkdir -p $O
-ARGS=${BENCH_ARGS:---no-global-leg --no-surface-leg}
+ARGS=${BENCH_ARGS:---no-global-leg --no-surface-leg --no-airplane-leg}
 for rep in $(seq 1 ${REPEAT:-1}); do
   for spec in "$@"; do
     name=${spec%%|*}; envs=${spec#*|}

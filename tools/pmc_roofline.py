@@ -25,10 +25,12 @@ tag = sys.argv[sys.argv.index("--tag") + 1] if "--tag" in sys.argv else out_dir.
 only = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else None
 root = pathlib.Path(__file__).resolve().parent.parent
 
+AIRPLANE_LEG = "torusknot262144_airplane_materials_1920x1080_64spp"  # bench.py's texture-sampling leg
 LEGS = {  # kernel instance -> the workloads bench.py runs on it, in launch order (one timed launch each)
     "void srt::sample_kernel<false, true, true, 1024, false, false, 4>": ["rubik_1920x1080_256spp"],
     "void srt::sample_kernel<false, false, true, 256, false, true, 4>": ["synthetic1000000_1920x1080_16spp"],
     "void srt::sample_kernel<false, false, true, 256, false, true, 5>": ["torusknot262144_1920x1080_64spp"],
+    "void srt::sample_kernel<false, false, true, 256, true, true, 5>": [AIRPLANE_LEG],
 }
 
 
@@ -82,7 +84,7 @@ def bench_code_hash(sub):
 
 
 sq, fetch, write = per_launch("pmc_sq"), per_launch("pmc_fetch"), per_launch("pmc_write")
-code = {bench_code_hash(s) for s in ("pmc_sq", "pmc_fetch", "pmc_write")}
+code = {bench_code_hash(s) for s in ("pmc_sq", "pmc_fetch", "pmc_write") + (("pmc_sq2",) if (out_dir / "pmc_sq2").exists() else ())}
 assert len(code) == 1, f"the passes profiled different code: {code}"
 code = code.pop()
 p = root / "profiles" / "counters.json"
@@ -92,6 +94,8 @@ for wl in sq:
     d["FETCH_SIZE"] = fetch[wl]["FETCH_SIZE"]
     d["WRITE_SIZE"] = write[wl]["WRITE_SIZE"]
     d["hbm_bytes"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
+    if (out_dir / "pmc_sq2").exists():  # issue and wave-state counters (tools/profile_round.sh's second SQ pass)
+        d.update({k: v for k, v in per_launch("pmc_sq2").get(wl, {}).items() if k not in d})
     if (out_dir / "pmc_tcc").exists():
         tcc = per_launch("pmc_tcc").get(wl, {})
         d.update({k: v for k, v in tcc.items()})

@@ -6,7 +6,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_wavefront.py -x -v --timeou
   > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $O/pytest.log; exit 1; }
 tail -3 $O/pytest.log
 run() {  # name, env, bench args
-  env $2 timeout -k 10 300 python bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-global-leg --no-surface-leg $3 \
+  env $2 timeout -k 10 300 python bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-global-leg --no-surface-leg --no-airplane-leg $3 \
     > $O/$1.json 2> $O/$1.err || { echo "$1 FAILED"; tail -5 $O/$1.err; exit 1; }
   python3 -c "import json,sys; d=json.load(open('$O/$1.json')); print('$1', d['config']['workload'], d['value'], 'Mrays/s kernel', d['roofline']['kernel_ms'], 'ms')" | tee -a $O/results.txt
 }
