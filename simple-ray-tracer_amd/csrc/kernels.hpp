@@ -42,6 +42,17 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
 #ifndef SRT_NT_SAMPLES
 #define SRT_NT_SAMPLES 0  // sample-buffer stores with the streaming (nontemporal) policy
 #endif
+#ifndef SRT_NT_JITTER
+#define SRT_NT_JITTER 0   // camera-jitter (noiseTex) loads with the streaming policy (an experiment, round 5)
+#endif
+// sphere_kernel streams its camera-jitter loads and sample-buffer stores past the XCD's L2 (round 5): each
+// is touched once per sample, and the L2 then holds the randomly gathered noiseUniformTex -- C2's L2 hit
+// rate 0.68 -> 0.79 and its L2-miss lines per sample 84.6 -> 54.5 B (§8d: 52.6 B) at the same kernel time
+// (profiles/r05_experiments/c2_streaming_policy.json); the mesh kernels lose 0.7-2% with it (their L2
+// holds tree lines too), so they keep the default policy
+#ifndef SRT_NT_SPH
+#define SRT_NT_SPH 1
+#endif
 // The IL instance (trees past 600 MB) deals a tile's frames in a row (C5 783 -> 771 ms per launch,
 // A/B on one box; 8 or 16 batches per claim instead of 4: 776 / 792 ms)
 #ifndef SRT_TILE_MAJOR_IL
@@ -356,14 +367,14 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
       atomicAdd(&kp.tile_cost[(ly >> 3) * tiles_x + (px >> 3)], (uint32_t)(bounces + 1));
     }
     color = color + T * mk(0.05f, 0.05f, 0.05f);  // skyColor, raytrace_compute.glsl:219,292
-#if SRT_NT_SAMPLES
-    // streaming store: the sample buffer passes through L2 once, and would evict the noise tables
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    const v4f v = {color.x, color.y, color.z, 0.0f};
-    __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(kp.lbuf + ((size_t)fidx * (size_t)kp.local_pixels + (size_t)li)));
-#else
-    kp.lbuf[(size_t)fidx * (size_t)kp.local_pixels + (size_t)li] = make_float4(color.x, color.y, color.z, 0.0f);
-#endif
+    if constexpr (SRT_NT_SAMPLES || (SPH && SRT_NT_SPH)) {
+      // streaming store: the sample buffer passes through L2 once, and would evict the noise tables
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      const v4f v = {color.x, color.y, color.z, 0.0f};
+      __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(kp.lbuf + ((size_t)fidx * (size_t)kp.local_pixels + (size_t)li)));
+    } else {
+      kp.lbuf[(size_t)fidx * (size_t)kp.local_pixels + (size_t)li] = make_float4(color.x, color.y, color.z, 0.0f);
+    }
     has_work = false;
   };
 
@@ -447,7 +458,16 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
       fidx = a_f;
       ln.base = gy * kp.H + x;
       // GetRay (raytrace_compute.glsl:78-90) with SampleSquare (raytrace_utils.glsl:10-17)
-      const float2 nz = kp.noise_xy[wrap_index(ln.base + a_samp, kp.WH)];
+      float2 nz;
+      if constexpr (SRT_NT_JITTER || (SPH && SRT_NT_SPH)) {
+        // the jitter texel streams past L2 (each is read once per sample), leaving the XCD's L2 to the
+        // randomly gathered uniform-noise table
+        typedef float v2f __attribute__((ext_vector_type(2)));
+        const v2f nzv = __builtin_nontemporal_load(reinterpret_cast<const v2f*>(kp.noise_xy) + wrap_index(ln.base + a_samp, kp.WH));
+        nz = make_float2(nzv.x, nzv.y);
+      } else {
+        nz = kp.noise_xy[wrap_index(ln.base + a_samp, kp.WH)];
+      }
       bump<COUNT>(c, ST_RNGSQ);
       bump<COUNT>(c, ST_SAMPLES);
       const f3 p00 = mk(kp.p00x, kp.p00y, kp.p00z);
