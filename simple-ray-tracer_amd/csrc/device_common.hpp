@@ -59,7 +59,8 @@ struct KParams {
   float cx, cy, cz, p00x, p00y, p00z, dux, duy, duz, dvx, dvy, dvz;
   // texture sampling (the TEX kernel instances)
   const float4* tri_uv;      // 2 float4 per triangle: vertex uvs uv0 uv1 | uv2
-  const float4* tex_texels;  // RGBA32F texels of all textures
+  const float4* tex_texels;  // RGBA32F texels of all textures (SRT_TEX8=0 builds)
+  const uint32_t* tex_texels8;  // RGBA8 texels of all textures, r | g << 8 | b << 16 (SRT_TEX8 builds)
   const uint4* tex_info;     // per texture: first texel, width, height
   uint32_t n_tex;
   // LDS copies of the light and material records (read per shading), when they fit

@@ -90,7 +90,7 @@ struct srt_context {
   uint32_t ref_or = 0;  // KParams::ref_or of the uploaded node layout
   // textures (srt_upload_textures) and, when materials sample them, the
   // per-triangle vertex uvs (2 float4: uv0 uv1 | uv2 0 0)
-  float4* d_tex = nullptr;
+  void* d_tex = nullptr;         // texels: RGBA8 (SRT_TEX8) or RGBA32F
   uint4* d_tex_info = nullptr;  // first texel, width, height, 0
   uint32_t n_tex = 0;
   float4* d_tri_uv = nullptr;
@@ -418,7 +418,8 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
   kp->tris = c->d_tris;
   kp->mats = c->d_mats;
   kp->tri_uv = c->d_tri_uv;
-  kp->tex_texels = c->d_tex;
+  kp->tex_texels = static_cast<const float4*>(c->d_tex);
+  kp->tex_texels8 = static_cast<const uint32_t*>(c->d_tex);
   kp->tex_info = c->d_tex_info;
   kp->n_tex = c->d_tex ? c->n_tex : 0u;
   kp->lights = c->d_lights;
@@ -1939,25 +1940,36 @@ int srt_upload_textures(srt_context* c, const srt_texture* textures, uint32_t n)
       return SRT_ERR_LIMIT;
     }
   }
-  // RGBA32F texels, c / 255 (unorm8); GL_RED reads (r, 0, 0), a 2-channel file (r, g, 0)
-  std::vector<float4> tx(std::max<size_t>(total, 1), make_float4(0, 0, 0, 0));
+  // GL_RED reads (r, 0, 0), a 2-channel file (r, g, 0); channel values are c / 255 (unorm8)
+#if SRT_TEX8
+  // the file's bytes, RGBA8 (the kernel's unorm8 reads c / 255 exactly): 4 B a texel
+  using Texel = uint32_t;
+  std::vector<Texel> tx(std::max<size_t>(total, 1), 0u);
+#else
+  using Texel = float4;  // RGBA32F, c / 255
+  std::vector<Texel> tx(std::max<size_t>(total, 1), make_float4(0, 0, 0, 0));
+#endif
   for (uint32_t i = 0; i < n; ++i) {
     const srt_texture& t = textures[i];
     const size_t m = (size_t)t.width * (size_t)t.height;
     for (size_t k = 0; k < m; ++k) {
       const uint8_t* p = t.texels + k * t.channels;
-      float v[4] = {0.0f, 0.0f, 0.0f, 1.0f};
-      for (int ch = 0; ch < t.channels && ch < 3; ++ch) v[ch] = (float)p[ch] / 255.0f;
-      if (t.channels == 2) v[2] = 0.0f;
-      tx[info[i].x + k] = make_float4(v[0], v[1], v[2], v[3]);
+      uint32_t v[3] = {0u, 0u, 0u};
+      for (int ch = 0; ch < t.channels && ch < 3; ++ch) v[ch] = p[ch];
+      if (t.channels == 2) v[2] = 0u;
+#if SRT_TEX8
+      tx[info[i].x + k] = v[0] | (v[1] << 8) | (v[2] << 16);
+#else
+      tx[info[i].x + k] = make_float4((float)v[0] / 255.0f, (float)v[1] / 255.0f, (float)v[2] / 255.0f, 1.0f);
+#endif
     }
   }
   HIP_OK(hipSetDevice(c->device));
   FreeDev(c->d_tex); FreeDev(c->d_tex_info);
   c->d_tex = nullptr; c->d_tex_info = nullptr; c->n_tex = 0;
-  HIP_OK(hipMalloc(&c->d_tex, tx.size() * sizeof(float4)));
+  HIP_OK(hipMalloc(&c->d_tex, tx.size() * sizeof(Texel)));
   HIP_OK(hipMalloc(&c->d_tex_info, info.size() * sizeof(uint4)));
-  HIP_OK(hipMemcpyAsync(c->d_tex, tx.data(), tx.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipMemcpyAsync(c->d_tex, tx.data(), tx.size() * sizeof(Texel), hipMemcpyHostToDevice, c->stream));
   HIP_OK(hipMemcpyAsync(c->d_tex_info, info.data(), info.size() * sizeof(uint4), hipMemcpyHostToDevice, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
   c->n_tex = n;

@@ -8,6 +8,20 @@
 namespace srt {
 using namespace dev;
 
+// Texels are kept as the file's bytes, RGBA8 (SRT_TEX8, round 5: 4 B a texel instead of 16), and a
+// channel c is read as c / 255 -- the contract's value, the correctly rounded quotient -- by q = c * RN(1/255)
+// and one Markstein correction q + (c - 255 q) / 255 with the residual exact in an FMA: equal to c / 255.0f
+// for all 256 values (checked exactly in tests/test_producers.py).
+#ifndef SRT_TEX8
+#define SRT_TEX8 1
+#endif
+__device__ __forceinline__ float unorm8(uint32_t p, int sh) {
+  constexpr float kInv255 = 0.003921568859368563f;  // RN(1 / 255)
+  const float c = (float)((p >> sh) & 255u);
+  const float q = c * kInv255;
+  return __builtin_fmaf(__builtin_fmaf(-255.0f, q, c), kInv255, q);
+}
+
 // texture(sampler2D, vec2(s, t)).xyz at level 0, GL_LINEAR, GL_REPEAT: the
 // sampling contract of scene.cpp TextureSample
 __device__ __forceinline__ f3 texture_sample(const KParams& kp, uint32_t tex, float s, float t) {
@@ -27,9 +41,19 @@ __device__ __forceinline__ f3 texture_sample(const KParams& kp, uint32_t tex, fl
   i1 = i1 >= w ? 0 : i1;
   j1 = j1 >= h ? 0 : j1;
   const float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+#if SRT_TEX8
+  const uint32_t* T = kp.tex_texels8 + info.x;
+  const uint32_t p00 = T[(uint32_t)j0 * w + i0], p10 = T[(uint32_t)j0 * w + i1];
+  const uint32_t p01 = T[(uint32_t)j1 * w + i0], p11 = T[(uint32_t)j1 * w + i1];
+  const f3 t00 = mk(unorm8(p00, 0), unorm8(p00, 8), unorm8(p00, 16));
+  const f3 t10 = mk(unorm8(p10, 0), unorm8(p10, 8), unorm8(p10, 16));
+  const f3 t01 = mk(unorm8(p01, 0), unorm8(p01, 8), unorm8(p01, 16));
+  const f3 t11 = mk(unorm8(p11, 0), unorm8(p11, 8), unorm8(p11, 16));
+#else
   const float4* T = kp.tex_texels + info.x;
   const float4 t00 = T[(uint32_t)j0 * w + i0], t10 = T[(uint32_t)j0 * w + i1];
   const float4 t01 = T[(uint32_t)j1 * w + i0], t11 = T[(uint32_t)j1 * w + i1];
+#endif
   return mk(((w00 * t00.x + w10 * t10.x) + w01 * t01.x) + w11 * t11.x,
             ((w00 * t00.y + w10 * t10.y) + w01 * t01.y) + w11 * t11.y,
             ((w00 * t00.z + w10 * t10.z) + w01 * t01.z) + w11 * t11.z);

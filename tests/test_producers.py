@@ -264,6 +264,23 @@ def test_texture_sampler_contract(w, h, ch):
     np.testing.assert_array_equal(c, np.float32(exp))
 
 
+def test_unorm8_read_is_the_correctly_rounded_quotient():
+    """The kernel keeps texels as RGBA8 and reads a channel c as q = c * RN(1/255) corrected once by
+    fma(fma(-255, q, c), RN(1/255), q) (shading.hpp unorm8): for every byte that is c / 255.0f, the value
+    the contract (and the host sampler above) uses.  fmaf from libm: one rounding, like the device's."""
+    import ctypes
+    fmaf = ctypes.CDLL("libm.so.6").fmaf
+    fmaf.argtypes = [ctypes.c_float] * 3
+    fmaf.restype = ctypes.c_float
+    f = np.float32
+    r = f(1) / f(255)
+    assert r == f(0.003921568859368563)
+    for c in range(256):
+        q = f(f(c) * r)
+        got = f(fmaf(fmaf(-255.0, q, float(c)), r, q))
+        assert got.view(np.uint32) == (f(c) / f(255)).view(np.uint32), c
+
+
 OBJ_UV = """mtllib m.mtl
 v 0 0 0
 v 1 0 0

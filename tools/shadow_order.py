@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Diagnostic: how many traversal steps a shadow ray takes under the reference's child order, nearer-first
-and farther-first (tools/shadow_order.c).  Shadow rays (CheckLightOccluded) only need CheckHit(...).hit,
+and farther-first (tools/shadow_order.c), and how many fused sub-steps (memory round trips) under the
+kernel's schedule and under schedules that expand the stack's top entry in the same step (tools/shadow_steps.c).  Shadow rays (CheckLightOccluded) only need CheckHit(...).hit,
 which does not depend on the visit order, so an any-hit walk may take either child first.
 
 The rays: the camera ray through each pixel centre of a W x H frame of the scene (model camera), its first
@@ -62,10 +63,11 @@ def main():
         f.write(tri.tobytes())
         f.write(sh.tobytes())
         path = f.name
-    exe = pathlib.Path(tempfile.gettempdir()) / "shadow_order"
-    subprocess.run(["gcc", "-O2", "-o", str(exe), str(ROOT / "tools" / "shadow_order.c"), "-lm"], check=True)
     print(f"{scene_name} {W}x{H}: {int(m.sum())} camera-ray hits x {len(lp)} lights = {len(sh)} shadow rays")
-    print(subprocess.run([str(exe), path], check=True, capture_output=True, text=True).stdout, end="")
+    for tool in ("shadow_order", "shadow_steps"):  # visit orders; fused sub-steps (round trips) per schedule
+        exe = pathlib.Path(tempfile.gettempdir()) / tool
+        subprocess.run(["gcc", "-O2", "-o", str(exe), str(ROOT / "tools" / f"{tool}.c"), "-lm"], check=True)
+        print(subprocess.run([str(exe), path], check=True, capture_output=True, text=True).stdout, end="")
     pathlib.Path(path).unlink()
 
 
