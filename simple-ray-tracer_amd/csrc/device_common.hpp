@@ -54,6 +54,7 @@ struct KParams {
   int pool_ctl_off, pool_ring_off, pool_rec_off, pool_cap, pool_slots, pool_batch, pool_tlow;
   unsigned long long pool_deadline;
   int stack_base_f4;       // first float4 of the per-lane stacks in dynamic LDS
+  int coop_off;            // global-scene mode, SRT_COOP: LDS byte offset of the waves' load stages (traversal.hpp)
   uint32_t* gstack;        // global-scene mode: per-lane stacks in HBM, entry field k of lane g at gstack[k * stride + g]
   int gstack_stride;       // lanes in the grid
   float cx, cy, cz, p00x, p00y, p00z, dux, duy, duz, dvx, dvy, dvz;

@@ -63,7 +63,8 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
 // spills; 16-entry LDS rings, 32 KiB per 256-lane block), or 5 (<= 96 VGPRs, ~10
 // dwords spilled; 8-entry rings, 16 KiB per block) for trees small enough that
 // more rays in flight beat the spills (srt_upload_scene picks it by scene size).
-__host__ __device__ constexpr int global_ring(int gw) { return gw > 4 ? 8 : kShortStack; }
+// (SRT_COOP builds keep 8-entry rings at either regime: the cooperative loads' stage takes the rest)
+__host__ __device__ constexpr int global_ring(int gw) { return (gw > 4 || SRT_COOP) ? 8 : kShortStack; }
 // GetRayColor's loop body for a ray whose CheckHit hit (raytrace_compute.glsl:225-290): the
 // hit record, this bounce's draws, SampleLights, both shadow outcomes of the direct light
 // (q0: occluded, q1: visible), the BRDF choice, Russian roulette and the next direction.
@@ -334,6 +335,10 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
   tr.active = false;
   tr.start = false;
   tr.hit = kNoneRef;
+  tr.cnt = kNoneCnt;  // (idle: a wave-wide step leaves such a lane alone)
+  tr.ref = 0;
+  tr.sp = 0;
+  tr.lo = 0;
 
 #ifdef SRT_PHASE_TIMING
   unsigned long long d_kind[6] = {0, 0, 0, 0, 0, 0};  // (ST_DBG_KIND)
@@ -514,7 +519,11 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
         d_leaf += __popcll(__ballot(tr.active && trav_at_leaf(tr.cnt)));
         d_int += __popcll(__ballot(tr.active && tr.cnt == 0));
 #endif
-        if (tr.active) trav_step<COUNT, LDSM, PACK, FUSE, global_ring(GW)>(kp, ln, c, tr, ro, rd, shadow_phase);
+        // (cooperative loads need every lane of the wave as a loader: the step runs wave-wide, and a lane
+        // with no ray is idle in it -- nothing current, an empty stack, no BVH to set up)
+        constexpr bool kCoopInst = (bool)SRT_COOP && FUSE && !LDSM;
+        if (kCoopInst || tr.active)
+          trav_step<COUNT, LDSM, PACK, FUSE, global_ring(GW), false, kCoopInst>(kp, ln, c, tr, ro, rd, shadow_phase);
       }
     }
 

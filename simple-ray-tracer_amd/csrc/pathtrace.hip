@@ -859,6 +859,11 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
       kp.stack_base_f4 = 0;
       const int gw = (!count && c->fused) ? c->global_waves : 4;  // LaunchMode's instance
       lds = (size_t)block * (c->lds_ok ? 2 : 3) * sizeof(uint32_t) * (size_t)srt::global_ring(gw);
+      if (SRT_COOP && !count && c->fused) {  // the fused sub-steps' load stages, one per wave
+        lds = (lds + 15) & ~(size_t)15;
+        kp.coop_off = (int)lds;
+        lds += (size_t)(block / 64) * srt::kCoopWaveBytes;
+      }
     } else {  // the sphere scene (sphere_kernel): no traversal stacks
       kp.stack_base_f4 = 0;
       lds = 0;

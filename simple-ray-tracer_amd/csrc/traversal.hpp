@@ -554,6 +554,88 @@ __device__ __forceinline__ void trav_internal(const KParams& kp, const Lane& ln,
 template <bool LDSM, bool PACK, int RING = kShortStack>
 __device__ __forceinline__ void trav_pop(const KParams& kp, const Lane& ln, Trav& t);
 
+// Cooperative line loads (global-scene mode, SRT_COOP).  The fused sub-step's loads are divergent
+// gathers: each lane reads its own 64-128 B with 4-8 dwordx4 instructions, and the vector-memory
+// pipeline (TA/TD) spends about one cycle per distinct cache line per instruction -- ~30 per
+// instruction, busy 0.93-0.97 of the kernel's time (profiles/r05_experiments/vmem_pipeline.json).
+// Instead, 8 lanes fetch one lane's request together: one instruction moves 8 requests' whole lines
+// (1 KB, 8 lines) by LDS-DMA into a per-wave stage, and each lane reads its own row back.  The active
+// lanes are ranked (mbcnt of the wave's ballot) and publish their request word in a rank table; a round
+// stages kCoopRows ranks (three groups of 8), so a sub-step with more active lanes takes a second
+// round.  Row r holds slot k at 16-B position (k + (r >> 1)) & 7, so 16 lanes reading the same slot
+// of consecutive rows hit 16 different 16-B bank slots.
+#ifndef SRT_COOP
+#define SRT_COOP 0
+#endif
+constexpr int kCoopRows = 24;
+constexpr uint32_t kCoopRowBytes = 128;                                          // 8 float4
+constexpr uint32_t kCoopWaveBytes = kCoopRows * kCoopRowBytes + 64 * 4;          // rows + rank table
+constexpr uint32_t kCoopIdxBits = 29;  // request word: float4 index | (nf4 / 2 - 2) << 29 | leaf << 31
+
+template <bool COUNT, bool PACK, int RING>
+__device__ __forceinline__ void trav_fused_coop(const KParams& kp, const Lane& ln, Counters& c, Trav& t, bool any) {
+  const bool at_int = t.cnt == 0u, at_leaf = trav_at_leaf(t.cnt);
+  const bool act = at_int | at_leaf;
+  const uint32_t ref0 = t.ref | kp.ref_or;
+  const bool spine = kSpine<false> && at_int && (ref0 != t.ref);
+  static_assert(kLeafTris == 2, "trav_fused_coop stages two triangle records");
+  const uint64_t M = __ballot(act);
+  const uint32_t n = (uint32_t)__popcll(M);  // wave-uniform
+  float4 x[8];
+  if (n != 0u) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t stage = (uint32_t)kp.coop_off + (threadIdx.x >> 6) * kCoopWaveBytes;  // wave-uniform
+    uint32_t* table = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(g_smem) + stage + kCoopRows * kCoopRowBytes);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
+    if (act) {
+      const uint32_t idx = at_leaf ? 3u * t.ref : 2u * ref0 + 2u;
+      const uint32_t cls = at_leaf ? 1u : (spine ? 2u : 0u);  // nf4 = 4 + 2 cls
+      table[rank] = idx | (cls << kCoopIdxBits) | ((at_leaf ? 1u : 0u) << 31);
+    }
+    for (uint32_t base = 0; base < n; base += (uint32_t)kCoopRows) {  // rounds (wave-uniform)
+      if (base != 0u) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last round's rows are read
+#pragma unroll
+      for (int j = 0; j < kCoopRows / 8; ++j) {
+        if (base + 8u * j < n) {  // wave-uniform
+          const uint32_t row = 8u * j + (lane >> 3), r = base + row;
+          if (r < n) {
+            const uint32_t w = table[r];
+            const uint32_t k = ((lane & 7u) - (row >> 1)) & 7u;  // the slot this lane's position holds
+            const uint32_t nf4 = 4u + 2u * ((w >> kCoopIdxBits) & 3u);
+            const float4* src = ((w >> 31) ? kp.tris : kp.nodes) + (w & ((1u << kCoopIdxBits) - 1u)) + k;
+            if (k < nf4)
+              __builtin_amdgcn_global_load_lds(
+                  (__attribute__((address_space(1))) void*)src,
+                  (__attribute__((address_space(3))) void*)((__attribute__((address_space(3))) char*)g_smem + stage +
+                                                            (uint32_t)j * 8u * kCoopRowBytes),
+                  16, 0, 0);
+          }
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (act && rank - base < (uint32_t)kCoopRows) {  // (unsigned: rank >= base)
+        const uint32_t row = rank - base, rot = row >> 1;
+        const uint32_t rb = stage + row * kCoopRowBytes;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = lds4(rb + (((uint32_t)k + rot) & 7u) * 16u);
+        if (at_leaf | spine) {
+          x[4] = lds4(rb + ((4u + rot) & 7u) * 16u);
+          x[5] = lds4(rb + ((5u + rot) & 7u) * 16u);
+        }
+        if (spine) {
+          x[6] = lds4(rb + ((6u + rot) & 7u) * 16u);
+          x[7] = lds4(rb + ((7u + rot) & 7u) * 16u);
+        }
+      }
+    }
+    if (at_int)
+      trav_internal_x<COUNT, false, PACK, RING>(kp, ln, c, t, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], spine);
+    else if (at_leaf)
+      trav_leaf_x<COUNT, false>(kp, c, t, any, x);
+  }
+  trav_pop<false, PACK, RING>(kp, ln, t);
+}
+
 // Global-scene mode: one sub-step for both node kinds.  Lanes at an internal
 // node and lanes at a leaf issue their loads (node pairs or triangle records)
 // as one set of per-lane-addressed loads, so the wave waits for memory once
@@ -633,13 +715,15 @@ __device__ __forceinline__ void trav_finish(const KParams& kp, Trav& t, bool any
   }
 }
 
-template <bool COUNT, bool LDSM, bool PACK, bool FUSE, int K, int RING = kShortStack, bool TL = false>
+template <bool COUNT, bool LDSM, bool PACK, bool FUSE, int K, int RING = kShortStack, bool TL = false,
+          bool COOP = false>
 __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln, Counters& c, Trav& t, bool any) {
   if constexpr (FUSE) {
     static_assert(!LDSM, "fused sub-steps are a global-scene mode schedule");
     if constexpr (K < kFusedSteps) {
-      trav_fused<COUNT, PACK, RING, TL>(kp, ln, c, t, any);
-      trav_substeps<COUNT, LDSM, PACK, FUSE, K + 1, RING, TL>(kp, ln, c, t, any);
+      if constexpr (COOP) trav_fused_coop<COUNT, PACK, RING>(kp, ln, c, t, any);
+      else trav_fused<COUNT, PACK, RING, TL>(kp, ln, c, t, any);
+      trav_substeps<COUNT, LDSM, PACK, FUSE, K + 1, RING, TL, COOP>(kp, ln, c, t, any);
     }
   } else if constexpr (step_kind<LDSM>(K) != 0) {
     if constexpr (step_kind<LDSM>(K) == 'I') {
@@ -651,7 +735,7 @@ __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln,
     }
     DBG_COUNT(kp.stats, ST_DBG_SUB + 3 * K + 2, t.active & (t.cnt == kNoneCnt));
     trav_pop<LDSM, PACK, RING>(kp, ln, t);
-    trav_substeps<COUNT, LDSM, PACK, FUSE, K + 1, RING, TL>(kp, ln, c, t, any);
+    trav_substeps<COUNT, LDSM, PACK, FUSE, K + 1, RING, TL, COOP>(kp, ln, c, t, any);
   }
 }
 
@@ -663,12 +747,13 @@ __device__ __forceinline__ void trav_substeps(const KParams& kp, const Lane& ln,
 // RING: global-scene mode's LDS ring entries per lane (a power of two).
 // TL (wavefront mode's top-level kernel): a current node whose count is kTreeletCnt is a treelet root of
 // the flagged node copy; no sub-step takes it (the caller suspends the ray there, wavefront.hpp).
-template <bool COUNT, bool LDSM, bool PACK, bool FUSE, int RING = kShortStack, bool TL = false>
+// COOP: the fused sub-steps' loads as cooperative line loads (trav_fused_coop; the caller stages them).
+template <bool COUNT, bool LDSM, bool PACK, bool FUSE, int RING = kShortStack, bool TL = false, bool COOP = false>
 __device__ __forceinline__ void trav_step(const KParams& kp, const Lane& ln, Counters& c, Trav& t, f3 ro, f3 rd,
                                           bool any) {
   static_assert((RING & (RING - 1)) == 0, "the LDS ring holds a power-of-two number of entries");
   if (t.start) trav_begin_bvh<COUNT, LDSM>(kp, c, t, ro, rd);  // only for BVHs after the first
-  trav_substeps<COUNT, LDSM, PACK, FUSE, 0, RING, TL>(kp, ln, c, t, any);
+  trav_substeps<COUNT, LDSM, PACK, FUSE, 0, RING, TL, COOP>(kp, ln, c, t, any);
   trav_finish(kp, t, any);
 }
 

@@ -29,9 +29,14 @@ SIMDS = 1024
 KERNEL = "void srt::sphere_kernel<false>"
 
 
-def counters(d: pathlib.Path, kernel: str = KERNEL) -> dict:
+VMEM_PASSES = ("pmc_ta1", "pmc_ta2", "pmc_td", "pmc_tcp1", "pmc_tcp2", "pmc_tcp3")  # tools/vmem_study.sh
+
+
+def counters(d: pathlib.Path, kernel: str = KERNEL, per_pass: dict | None = None) -> dict:
+    """The timed launch's counters, merged over the passes (GRBM_GUI_ACTIVE from the first pass holding it;
+    `per_pass` receives each pass's own counters, for ratios against that pass's cycles)."""
     out = {}
-    for sub in ("pmc_sq", "pmc_sq2", "pmc_cyc", "pmc_fetch", "pmc_write", "pmc_tcc", "pmc_tcp"):
+    for sub in ("pmc_sq", "pmc_sq2", "pmc_cyc", "pmc_fetch", "pmc_write", "pmc_tcc", "pmc_tcp") + VMEM_PASSES:
         p = d / sub / "run_counter_collection.csv"
         if not p.exists():
             continue
@@ -40,10 +45,55 @@ def counters(d: pathlib.Path, kernel: str = KERNEL) -> dict:
         if not ids:
             continue
         last = ids[-1]  # the timed launch (the counting run is sphere_kernel<true>)
+        mine = {}
         for r in rows:
             if int(r["Dispatch_Id"]) == last:
-                out[r["Counter_Name"]] = out.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+                mine[r["Counter_Name"]] = mine.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        if per_pass is not None:
+            per_pass[sub] = mine
+        for k, v in mine.items():
+            if k == "GRBM_GUI_ACTIVE" and k in out:
+                continue
+            out[k] = v
     return out
+
+
+CUS = 256
+
+
+def vmem_ratios(pp: dict) -> dict:
+    """Vector-memory pipeline shares per pass (each against its own cycles, GRBM_GUI_ACTIVE / 8 XCDs):
+    ta_busy / td_busy (TA_TA_BUSY, TD_TD_BUSY over 256 CUs x cycles), the TA's cycles stalled on the
+    TCP for addresses / data, TD stalled on the TC, the mean L1 -> L2 read latency (cycles per request),
+    the UTCL1 translation miss rate and the TCP's stall shares."""
+    e = {}
+
+    def cyc(sub):
+        return pp.get(sub, {}).get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+
+    ta1, ta2, td = pp.get("pmc_ta1", {}), pp.get("pmc_ta2", {}), pp.get("pmc_td", {})
+    if ta1 and cyc("pmc_ta1"):
+        e["ta_busy"] = ta1["TA_TA_BUSY_sum"] / (CUS * cyc("pmc_ta1"))
+        e["ta_addr_stalled_by_tc"] = ta1["TA_ADDR_STALLED_BY_TC_CYCLES_sum"] / max(ta1["TA_TA_BUSY_sum"], 1.0)
+    if ta2 and cyc("pmc_ta2"):
+        e["ta_data_stalled_by_tc"] = ta2["TA_DATA_STALLED_BY_TC_CYCLES_sum"] / (CUS * cyc("pmc_ta2"))
+        e["ta_flat_read_wavefronts"] = ta2["TA_FLAT_READ_WAVEFRONTS_sum"]
+    if td and cyc("pmc_td"):
+        e["td_busy"] = td["TD_TD_BUSY_sum"] / (CUS * cyc("pmc_td"))
+        e["td_tc_stall"] = td["TD_TC_STALL_sum"] / (CUS * cyc("pmc_td"))
+    t1, t2, t3 = pp.get("pmc_tcp1", {}), pp.get("pmc_tcp2", {}), pp.get("pmc_tcp3", {})
+    if t1:
+        e["l2_read_latency_cyc"] = t1["TCP_TCC_READ_REQ_LATENCY_sum"] / max(t1["TCP_TCC_READ_REQ_sum"], 1.0)
+        e["tcp_pending_stall_cyc"] = t1["TCP_PENDING_STALL_CYCLES_sum"]
+        e["tcp_tcr_stall_cyc"] = t1["TCP_TCR_TCP_STALL_CYCLES_sum"]
+    if t2:
+        e["utcl1_miss_rate"] = t2["TCP_UTCL1_TRANSLATION_MISS_sum"] / max(t2["TCP_UTCL1_REQUEST_sum"], 1.0)
+        e["tcp_read_tagconflict_stall_cyc"] = t2["TCP_READ_TAGCONFLICT_STALL_CYCLES_sum"]
+    if t3:
+        e["tcp_latency_cyc_per_access"] = t3["TCP_TCP_LATENCY_sum"] / max(t3["TCP_TOTAL_CACHE_ACCESSES_sum"], 1.0)
+        e["tcp_ta_data_stall_cyc"] = t3["TCP_TCP_TA_DATA_STALL_CYCLES_sum"]
+        e["tcp_accesses"] = t3["TCP_TOTAL_CACHE_ACCESSES_sum"]
+    return e
 
 
 def main():
@@ -58,7 +108,8 @@ def main():
         n = d.name[1:] if not study else d.name
         bench = json.loads((d / "bench.json").read_text())
         k_ms = bench["roofline"]["kernel_ms"]
-        c = counters(d, kernel)
+        pp = {}
+        c = counters(d, kernel, pp)
         cfg = bench["config"]
         samples = cfg["width"] * cfg["height"] * cfg["spp"]
         e = {"variant": n, "kernel_ms": k_ms, "Mrays_s": bench["value"], "rays": bench["rays_per_step"],
@@ -93,12 +144,17 @@ def main():
         if "WRITE_SIZE" in c:
             e["write_B"] = c["WRITE_SIZE"] * 1024
             e["write_B_per_sample"] = e["write_B"] / samples
+        e.update(vmem_ratios(pp))
+        if "tcp_accesses" in e and "SQ_INSTS_VMEM_RD" in c:
+            e["tcp_accesses_per_vmem_rd"] = e["tcp_accesses"] / max(c["SQ_INSTS_VMEM_RD"], 1.0)
         res["by_blocks"][str(n)] = e
     outp.write_text(json.dumps(res, indent=1) + "\n")
     keys = ("kernel_ms", "valu_issue", "valu_busy", "cycles_per_valu", "valu2_share", "sca_busy", "trans_share",
             "f64_share", "lane_util", "wait_any", "wait_inst", "active_inst", "l2_hit",
             "l1_miss_req_frac", "fetch_lines_B_per_sample", "write_B_per_sample", "sq_insts_valu_per_ray",
-            "sq_insts_salu_per_ray", "sq_insts_vmem_rd_per_ray", "sq_insts_lds_per_ray")
+            "sq_insts_salu_per_ray", "sq_insts_vmem_rd_per_ray", "sq_insts_lds_per_ray", "ta_busy",
+            "ta_addr_stalled_by_tc", "ta_data_stalled_by_tc", "td_busy", "td_tc_stall", "l2_read_latency_cyc",
+            "utcl1_miss_rate", "tcp_latency_cyc_per_access", "tcp_accesses_per_vmem_rd")
     print("blocks " + " ".join(keys))
     for n, e in res["by_blocks"].items():
         print(n, " ".join(f"{e.get(k, float('nan')):.4g}" if isinstance(e.get(k), (int, float)) else "-" for k in keys))
