@@ -239,8 +239,7 @@ int srt_upload_scene(srt_context* ctx,
 /* GPUTexture(file, true) + GetHandle() (gpu_texture.h:24-68,133-137): the
  * textures sampled by use_texture materials; texture i gets handle i.
  * Replaces any previous set.  Sampling contract:
- * level 0, GL_LINEAR, GL_REPEAT, texels c/255 (kept on the device as the
- * file's bytes, 4 B a texel, and read as c/255 exactly). */
+ * level 0, GL_LINEAR, GL_REPEAT, texels c/255. */
 int srt_upload_textures(srt_context* ctx, const srt_texture* textures, uint32_t n);
 /* The same sampler on the host: texture(sampler2D, vec2(s, t)).xyz. */
 int srt_texture_sample(const srt_texture* tex, float s, float t, float rgb[3]);
