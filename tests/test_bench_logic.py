@@ -61,3 +61,20 @@ def test_counters_of_other_code_give_no_roof(monkeypatch):
     monkeypatch.setattr(bench, "load_counters", lambda wl: dict(CNT))
     rf = bench.roofline("rubik_1920x1080_256spp", 145.7, 10, "k")
     assert rf["frac"] is None and rf["counters_code_hash"] == "h"
+
+
+def test_committed_counters_are_for_the_sources():
+    """profiles/counters.json must hold counters of the code the sources build: every workload's code_hash
+    equals the hash the product build stamps (Makefile `hash`: kernel sources, srt_amd.h and the hipcc
+    flags).  A kernel edit without a re-capture (tools/gpu_round_profiles.sh) would leave the bench line
+    without roofs."""
+    import json
+    import pathlib
+    import subprocess
+
+    root = pathlib.Path(__file__).resolve().parent.parent
+    want = subprocess.run(["make", "-s", "-C", str(root / "simple-ray-tracer_amd"), "hash"], check=True,
+                          capture_output=True, text=True).stdout.strip()
+    counters = json.loads((root / "profiles" / "counters.json").read_text())
+    assert counters and all(v["code_hash"] == want for v in counters.values()), \
+        {k: v["code_hash"] for k, v in counters.items()}
