@@ -74,7 +74,9 @@ def l2_miss_peak_gbs() -> float:
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    # (10 timed steps: the first timed launch has no predecessor to overlap its drain, which 3 steps of a
+    # 26-ms leg would still show; the metric's 10 steps take 1.5 s)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", default="rubik", choices=("rubik", "spheres", "synthetic", "torusknot", "airplane_knot"))
     ap.add_argument("--width", type=int, default=1920)

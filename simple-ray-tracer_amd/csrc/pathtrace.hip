@@ -132,7 +132,7 @@ struct srt_context {
   int batch_ctr_cap = 0;
   size_t lbuf_bytes = 0;
   // SRT_SAMPLE_BUFFER_MB: every sample buffer of the context together (its own, used by counting and
-  // unpipelined launches, and one per pipeline slot), split equally: 16 GiB each with the 3 default slots
+  // unpipelined launches, and one per pipeline slot), split equally: 21 GiB each with the 2 default slots
   size_t lbuf_total = (size_t)64 << 30;
   int tail_claims = 16;  // SRT_TAIL_CLAIMS: claims per wave before the end from which claims take one batch
   int tail_claims_sph = 1;  // the sphere launch's (C2, 8 per claim: tail 16 6.20 ms, 1 3.17 ms; its batches
@@ -214,7 +214,10 @@ struct srt_context {
     size_t gstack_bytes = 0;
   };
   std::vector<Slot> slots;
-  int pipe = 3;                    // SRT_PIPELINE
+  // SRT_PIPELINE: launch slots, each its own stream and buffers.  Two, since launches overlap: a third slot's
+  // stream shares one of the process's 4 hardware queues (GPU_MAX_HW_QUEUES) with another, which serialises
+  // them (C2 52 -> 57 G rays/s, torus knot +2.8%, metric +0.2% with 2)
+  int pipe = 2;
   // SRT_PIPELINE_OVERLAP: whether a sample launch may start before the previous one ends (2, the default:
   // always; 1: on a rank's share of a multi-GPU split (nranks > 1) only; 0: never).  An overlapped launch's
   // dispatch-to-end time (rocprofv3) and span include its wait for the CUs other launches hold, so kernel
