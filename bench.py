@@ -56,6 +56,35 @@ VALU_PEAK_GIPS = SIMDS * CLOCK_HZ / VALU_ISSUE_CYCLES / 1e9  # 1228.8 G wave-ins
 LDS_PEAK_GCPS = CUS * CLOCK_HZ / 1e9  # 614.4 G LDS-array cycles/s (one per CU per clock)
 
 
+def valu_issue_calibrated_gips(waves: int):
+    """The VALU issue rate a SIMD reaches with `waves` waves of independent f32 arithmetic (tools/valu_issue_probe.hip,
+    profiles/r05_calib/valu_issue_calibration.json): the fastest of the FMA / MUL / ADD forms at the nearest measured
+    occupancy at or above `waves` (4 or 8 waves per SIMD), in G wave-instructions/s over 1024 SIMDs at 2.4 GHz.
+    Two VALU instructions may issue per quad-cycle only from different waves, and on gfx950 even independent
+    FMA streams reach 0.36-0.42 per cycle, not the nominal 0.5; min/max, compares and selects ~0.22."""
+    p = ROOT / "profiles" / "r05_calib" / "valu_issue_calibration.json"
+    try:
+        rows = json.loads(p.read_text())["rows"]
+        occ = min((r["waves_per_simd"] for r in rows if r["waves_per_simd"] >= waves), default=None)
+        if occ is None:
+            return None
+        rate = max(r["wave_instr_per_simd_per_cycle"] for r in rows if r["waves_per_simd"] == occ and
+                   r["form"].split()[0] in ("v_fmac_f32_e32", "v_fma_f32", "v_mul_f32_e32", "v_mul_f32_e64",
+                                            "v_sub_f32_e32"))
+        return {"peak": round(rate * SIMDS * CLOCK_HZ / 1e9, 1), "waves_per_simd_measured": occ,
+                "rate_per_simd_cycle": rate}
+    except Exception:
+        return None
+
+
+def kernel_waves(kernel_name: str) -> int:
+    """Waves per SIMD of the timed instance (timed_kernel()'s description; the LDS kernel runs 4)."""
+    import re
+
+    m = re.search(r"(\d+) waves per SIMD", kernel_name)
+    return int(m.group(1)) if m else 4
+
+
 def l2_miss_peak_gbs() -> float:
     """The memory-side roof for the traversal's reads, measured (tools/gather_calib.hip,
     profiles/r03_gather_calibration.json): every L2 miss is one 128-B line request (FETCH_SIZE tallies
@@ -212,6 +241,7 @@ def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str, globa
         "useful_valu_frac": round(fr["valu_issue"] * cnt["SQ_THREAD_CYCLES_VALU"] / (64.0 * cnt["SQ_INSTS_VALU"]), 4),
         "lds_bank_conflict_frac": round(cnt["SQ_LDS_BANK_CONFLICT"] / max(cnt["SQ_LDS_IDX_ACTIVE"], 1.0), 4),
         **issue_split(cnt, k_s),
+        **valu_calibrated(valu_gips, kernel_name),
         "counters_source": cnt.get("source", ""),
         "counters_code_hash": cnt.get("code_hash"),
         "note": "frac = the bound roof's fraction at the live kernel time; per-launch counters from the committed "
@@ -225,6 +255,20 @@ def roofline(workload: str, k_ms: float, alg_bytes: int, kernel_name: str, globa
                          "and the noise from L2, so it is not an HBM rate."),
     })
     return r
+
+
+def valu_calibrated(valu_gips: float, kernel_name: str) -> dict:
+    """The VALU issue fraction against the measured issue rate of independent f32 arithmetic at the instance's
+    occupancy (valu_issue_calibrated_gips), beside the nominal one (`fractions.valu_issue`)."""
+    cal = valu_issue_calibrated_gips(kernel_waves(kernel_name))
+    if not cal:
+        return {}
+    return {"valu_issue_calibrated": {"achieved": round(valu_gips, 2), "peak": cal["peak"],
+                                      "unit": "G VALU wave-instructions/s", "frac": round(valu_gips / cal["peak"], 4),
+                                      "waves_per_simd": kernel_waves(kernel_name),
+                                      "basis": f"independent f32 FMA/MUL streams at {cal['waves_per_simd_measured']} "
+                                               f"waves per SIMD: {cal['rate_per_simd_cycle']} wave-instructions per "
+                                               "SIMD per cycle (profiles/r05_calib/valu_issue_calibration.json)"}}
 
 
 def issue_split(cnt: dict, k_s: float) -> dict:

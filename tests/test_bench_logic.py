@@ -78,3 +78,16 @@ def test_committed_counters_are_for_the_sources():
     counters = json.loads((root / "profiles" / "counters.json").read_text())
     assert counters and all(v["code_hash"] == want for v in counters.values()), \
         {k: v["code_hash"] for k, v in counters.items()}
+
+
+def test_valu_issue_against_the_calibrated_rate(stub):
+    """The line also gives the VALU issue against the rate independent f32 arithmetic reaches at the instance's
+    occupancy (profiles/r05_calib/valu_issue_calibration.json, tools/valu_issue_probe.hip): the 4-wave LDS kernel
+    against the 4-wave rate, a 5-wave instance against the next measured occupancy (8)."""
+    rf = bench.roofline("rubik_1920x1080_256spp", 145.7, 10, bench.KERNEL_LDS)
+    cal = rf["valu_issue_calibrated"]
+    assert cal["waves_per_simd"] == 4 and cal["peak"] < bench.VALU_PEAK_GIPS
+    assert cal["frac"] == pytest.approx(rf["fractions"]["valu_issue"] * bench.VALU_PEAK_GIPS / cal["peak"], rel=1e-3)
+    g = bench.roofline("torusknot262144_1920x1080_64spp", 26.2, 10,
+                       "srt::sample_kernel<...> (global-scene mode, fused sub-steps, 5 waves per SIMD)", global_mode=True)
+    assert g["valu_issue_calibrated"]["waves_per_simd"] == 5 and "8 waves" in g["valu_issue_calibrated"]["basis"]
