@@ -54,10 +54,14 @@ typedef struct { uint32_t ref, cnt; } Ent;  /* internal: ref = node index, cnt =
 static const Node* g_nodes;
 static const float* g_tris;
 static double g_pairs, g_tests;
+static unsigned char* g_depth;       /* depth of each node (root 0) */
+static double g_pairs_by_depth[64];  /* node pairs expanded, by the depth of the expanded node (schedule 0) */
+static int g_sched;
 
 /* Expands internal node `n`: the children that pass go to *cur (c1 first) and the stack. */
 static void expand(uint32_t n, const float* o, const float* inv, float dist, Ent* cur, int* has, Ent* stk, int* sp) {
   g_pairs += 1;
+  if (g_sched == 0) g_pairs_by_depth[g_depth[n] < 63 ? g_depth[n] : 63] += 1;
   const uint32_t c0 = g_nodes[n].first, c1 = c0 + 1;
   const int v0 = box(&g_nodes[c0], o, inv) < dist, v1 = box(&g_nodes[c1], o, inv) < dist;
   Ent e0 = {g_nodes[c0].count ? g_nodes[c0].first : c0, g_nodes[c0].count};
@@ -82,7 +86,12 @@ int main(int argc, char** argv) {
   fclose(fp);
   g_nodes = nodes;
   g_tris = tris;
+  g_depth = calloc(hd[0], 1);
+  for (uint32_t i = 0; i < hd[0]; ++i)  /* children follow their parent in the array's pair order: one pass */
+    if (nodes[i].count == 0 && nodes[i].first + 1 < hd[0])
+      g_depth[nodes[i].first] = g_depth[nodes[i].first + 1] = (unsigned char)(g_depth[i] + 1);
   for (int sched = 0; sched < 3; ++sched) {
+    g_sched = sched;
     double steps = 0;
     long occl = 0;
     g_pairs = g_tests = 0;
@@ -151,6 +160,16 @@ int main(int argc, char** argv) {
     }
     printf("schedule %d: rays %u occluded %.4f sub-steps %.3f node pairs %.3f triangle tests %.3f per ray\n", sched,
            hd[2], (double)occl / hd[2], steps / hd[2], g_pairs / hd[2], g_tests / hd[2]);
+  }
+  {  /* node pairs expanded by depth (schedule 0), cumulative share: what an LDS copy of the top levels would serve */
+    double tot = 0, acc = 0;
+    for (int d = 0; d < 64; ++d) tot += g_pairs_by_depth[d];
+    printf("node pairs by depth of the expanded node, cumulative share:");
+    for (int d = 0; d < 24 && tot > 0; ++d) {
+      acc += g_pairs_by_depth[d];
+      printf(" %d:%.3f", d, acc / tot);
+    }
+    printf("\n");
   }
   return 0;
 }
