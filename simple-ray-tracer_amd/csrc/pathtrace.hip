@@ -1922,6 +1922,11 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   for (uint32_t i = 0; i < n_nodes; ++i)
     if (reach[i]) max_leaf = std::max(max_leaf, nodes[i].prim_count);
   c->lds_ok = n_tslots < (1u << 24) && n_slots + srt::kNodePad < (1u << 24) && max_leaf < 256;
+  // cooperative loads (SRT_COOP builds) carry a request's float4 index in kCoopIdxBits bits: larger
+  // arrays (only reachable with SRT_GLOBAL_FUSED_MODE=1 past 600 MB) take the IL instance
+  if (SRT_COOP && (2ull * ((uint64_t)c->n_nodes + 1) + 8 >= (1ull << srt::kCoopIdxBits) ||
+                   3ull * ((uint64_t)n_tslots + srt::kTriPad) >= (1ull << srt::kCoopIdxBits)))
+    c->fused = false;
   c->pairs_aligned = pairs_aligned;
   c->scene_ok = true;
   if (c->bvh_count == 0) c->bvh_count = n_bvhs;
