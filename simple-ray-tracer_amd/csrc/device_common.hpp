@@ -55,6 +55,10 @@ struct KParams {
   unsigned long long pool_deadline;
   int stack_base_f4;       // first float4 of the per-lane stacks in dynamic LDS
   int coop_off;            // global-scene mode, SRT_COOP: LDS byte offset of the waves' load stages (traversal.hpp)
+  // global-scene mode, fused instance: the node array's first top_f4 float4 (the top levels' pairs,
+  // pathtrace.hip LayoutNodes) copied into each block's LDS at float4 top_lds_f4 (padded pair blocks,
+  // node_lds_f4); 0: none
+  int top_f4, top_lds_f4;
   uint32_t* gstack;        // global-scene mode: per-lane stacks in HBM, entry field k of lane g at gstack[k * stride + g]
   int gstack_stride;       // lanes in the grid
   float cx, cy, cz, p00x, p00y, p00z, dux, duy, duz, dvx, dvy, dvz;

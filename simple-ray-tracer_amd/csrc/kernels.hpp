@@ -275,6 +275,9 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
     for (int i = tid; i < kp.nodes_f4; i += blockDim.x) g_smem[node_lds_f4((uint32_t)i)] = kp.nodes[i];
     for (int i = tid; i < kp.tris_f4; i += blockDim.x) g_smem[kp.nodes_lds_f4 + i] = kp.tris[i];
   }
+  if constexpr (FUSE && !LDSM) {  // global-scene mode: the top levels' pairs (kp.top_f4 float4, padded blocks)
+    for (int i = tid; i < kp.top_f4; i += blockDim.x) g_smem[kp.top_lds_f4 + (int)node_lds_f4((uint32_t)i)] = kp.nodes[i];
+  }
   {  // and the light and material records, when they fit (shading reads them from LDS)
     const int nl = kp.lights_lds ? 2 * (kp.light_records + 1) : 0, nm = kp.mats_lds ? 2 * kp.mat_records : 0;
     for (int i = tid; i < nl; i += blockDim.x) g_smem[kp.lights_base_f4 + i] = kp.lights[i];

@@ -101,6 +101,8 @@ struct srt_context {
   bool pairs_aligned = false; // every internal node's child pair starts at an odd slot (LDS mode's node_pair)
   bool force_global = false;  // SRT_FORCE_GLOBAL_SCENE=1 disables LDS mode
   bool fused = false;         // global-scene mode's fused sub-steps (set at upload: trees the Infinity Cache holds)
+  int top_f4 = 0, top_depth = 0;  // the node array's top-level region (LayoutNodes) the fused instance copies to LDS
+  int launch_top_f4 = 0;           // the region the last global-scene launch copied (0: none)
   int global_waves = 4;       // the fused instance's waves per SIMD (set at upload: 5 for small trees)
   // lights
   std::vector<srt_light> h_lights;
@@ -421,6 +423,8 @@ int FillParams(srt_context* c, srt::KParams* kp, bool need_images) {
   kp->tris = c->d_tris;
   kp->mats = c->d_mats;
   kp->tri_uv = c->d_tri_uv;
+  kp->top_f4 = 0;  // (set per launch: the fused instance's LDS copy of the top levels)
+  kp->top_lds_f4 = 0;
   kp->tex_texels = static_cast<const float4*>(c->d_tex);
   kp->tex_texels8 = static_cast<const uint32_t*>(c->d_tex);
   kp->tex_info = c->d_tex_info;
@@ -867,6 +871,21 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
         kp.coop_off = (int)lds;
         lds += (size_t)(block / 64) * srt::kCoopWaveBytes;
       }
+      // the top levels' pairs (LayoutNodes' first region) for the fused instance, when they fit beside the
+      // rings within the LDS one of the instance's gw blocks per CU may take (2 KB left for lights and
+      // materials); wavefront mode's kernels read none
+      kp.top_f4 = 0;
+      const bool wf_launch = !count && (c->wavefront >= 0 ? c->wavefront == 1 : c->wf_scene);
+      if (!count && c->fused && !wf_launch && c->top_f4 > 0) {
+        lds = (lds + 15) & ~(size_t)15;
+        const size_t tb = ((size_t)c->top_f4 + 3) / 4 * srt::kNodeBlkF4 * sizeof(float4);
+        if (lds + tb + 2048 <= kLdsBytes / (size_t)gw) {
+          kp.top_f4 = c->top_f4;
+          kp.top_lds_f4 = (int)(lds / sizeof(float4));
+          lds += tb;
+        }
+      }
+      c->launch_top_f4 = kp.top_f4;
     } else {  // the sphere scene (sphere_kernel): no traversal stacks
       kp.stack_base_f4 = 0;
       lds = 0;
@@ -1166,8 +1185,13 @@ int ValidateNodes(const srt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_tris, 
 // reference-built tree has.  A child pair reached from two BVH records' trees
 // keeps its first placement; srt_upload_scene sets a node's "right child's
 // pair follows" flag only where the remapped slots confirm it.
+// `top_depth` > 0 (global-scene scenes, SRT_TOP_DEPTH): the pairs of every node at depth < top_depth are
+// laid out first, in the same order, so they form the array's first `*n_top_slots` slots -- the region the
+// fused instance copies into each block's LDS (traversal.hpp trav_fused) -- and the rest follows.  A pair
+// on the region's last level keeps no right-spine flag (its right child's pair lies past the region).
 bool LayoutNodes(const srt_bvh_node* nodes, uint32_t n_nodes, const srt_bvh_record* bvhs, uint32_t n_bvhs,
-                 bool align, std::vector<uint32_t>* remap, uint32_t* n_slots) {
+                 bool align, std::vector<uint32_t>* remap, uint32_t* n_slots, int top_depth = 0,
+                 uint32_t* n_top_slots = nullptr) {
   constexpr uint32_t kUnset = 0xFFFFFFFFu;
   remap->assign(n_nodes, kUnset);
   auto& m = *remap;
@@ -1186,28 +1210,42 @@ bool LayoutNodes(const srt_bvh_node* nodes, uint32_t n_nodes, const srt_bvh_reco
   // 4: a zero pair pads before it when needed), so a step that reads a pair and
   // its right child's pair touches one line (see srt_upload_scene for when).
   uint32_t chain_next = kUnset;  // the node whose pair continues the current chain
-  std::vector<uint32_t> st;
-  for (uint32_t r : roots) {
-    st.push_back(r);
-    while (!st.empty()) {
-      const uint32_t i = st.back();
-      st.pop_back();
-      const srt_bvh_node& n = nodes[i];
-      if (n.prim_count > 0) continue;
-      const uint32_t c0 = n.first_child_or_prim_index, c1 = c0 + 1;
-      if (m[c0] == kUnset && m[c1] == kUnset) {
-        if (align && i != chain_next && nodes[c1].prim_count == 0 && (next & 3u) != 3u) next += 2;
-        m[c0] = next;
-        m[c1] = next + 1;
-        next += 2;
-        chain_next = nodes[c1].prim_count == 0 ? c1 : kUnset;
-        st.push_back(c0);  // popped after c1's subtree: c1 is visited first
-        st.push_back(c1);
-      } else if (m[c0] == kUnset || m[c1] != m[c0] + 1) {
-        return false;  // a shared or overlapping pair
+  std::vector<uint8_t> top(top_depth > 0 ? n_nodes : 0, 0);  // nodes whose pair the first pass laid out
+  std::vector<std::pair<uint32_t, int>> st;                    // (node, depth)
+  for (int pass = top_depth > 0 ? 0 : 1; pass < 2; ++pass) {
+    chain_next = kUnset;
+    for (uint32_t r : roots) {
+      st.push_back({r, 0});
+      while (!st.empty()) {
+        const uint32_t i = st.back().first;
+        const int d = st.back().second;
+        st.pop_back();
+        const srt_bvh_node& n = nodes[i];
+        if (n.prim_count > 0) continue;
+        const uint32_t c0 = n.first_child_or_prim_index, c1 = c0 + 1;
+        if (pass == 1 && !top.empty() && top[i]) {  // laid out by the first pass: descend only
+          st.push_back({c0, d + 1});
+          st.push_back({c1, d + 1});
+          continue;
+        }
+        if (pass == 0 && d >= top_depth) continue;
+        if (m[c0] == kUnset && m[c1] == kUnset) {
+          if (align && i != chain_next && nodes[c1].prim_count == 0 && (next & 3u) != 3u) next += 2;
+          m[c0] = next;
+          m[c1] = next + 1;
+          next += 2;
+          if (pass == 0) top[i] = 1;
+          chain_next = nodes[c1].prim_count == 0 ? c1 : kUnset;
+          st.push_back({c0, d + 1});  // popped after c1's subtree: c1 is visited first
+          st.push_back({c1, d + 1});
+        } else if (m[c0] == kUnset || m[c1] != m[c0] + 1) {
+          return false;  // a shared or overlapping pair
+        }
       }
     }
+    if (pass == 0 && n_top_slots) *n_top_slots = next;
   }
+  if (top_depth <= 0 && n_top_slots) *n_top_slots = 0;
   *n_slots = next;
   return true;
 }
@@ -1479,6 +1517,9 @@ int srt_get_int(srt_context* c, const char* name, int* v) {
   else if (n == "resetAccumBuffer") *v = c->reset;
   else if (n == "showModel") *v = c->show_model;
   else if (n == "scene.fused") *v = c->fused ? 1 : 0;
+  else if (n == "scene.top_depth") *v = c->top_depth;  // levels in the fused instance's LDS copy (0: none)
+  else if (n == "scene.top_f4") *v = c->top_f4;
+  else if (n == "launch.top_f4") *v = c->launch_top_f4;
   else if (n == "scene.global_waves") *v = c->global_waves;
   else if (n == "scene.wavefront") *v = c->wavefront >= 0 ? c->wavefront : (c->wf_scene ? 1 : 0);
   else if (n == "scene.wf_waves") *v = c->wf_waves;
@@ -1723,7 +1764,31 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   // Crossover taken at 48 MB; SRT_GLOBAL_WAVES_MODE=4/5 forces either.
   const char* gw_env = std::getenv("SRT_GLOBAL_WAVES_MODE");
   c->global_waves = gw_env ? (gw_env[0] == '5' ? 5 : 4) : (scene_mb < 48.0 ? 5 : 4);
-  bool laid = !(lay_env && lay_env[0] == '0') && LayoutNodes(nodes, n_nodes, bvhs, n_bvhs, align, &remap, &n_slots);
+  // The fused instance's LDS copy of the tree's top levels (traversal.hpp trav_fused): LDS reads bypass
+  // the vector-memory pipeline that bounds these kernels.  Laid out first, as deep
+  // as fits the LDS one block may take beside its rings (SRT_TOP_DEPTH=d forces d levels, 0 none).
+  uint32_t n_top = 0;
+  int top_depth = 0;
+  {
+    const char* td_env = std::getenv("SRT_TOP_DEPTH");
+    if (c->fused && scene_mb >= 1.0 && !(td_env && std::atoi(td_env) <= 0)) {
+      const bool pack = 3ull * n_tris < (1ull << 24) && (uint64_t)n_nodes + srt::kNodePad < (1ull << 24);
+      const size_t ring = (size_t)256 * (pack ? 2 : 3) * sizeof(uint32_t) * (size_t)srt::global_ring(c->global_waves);
+      const size_t budget = kLdsBytes / (size_t)c->global_waves - ring - 2048;
+      top_depth = td_env ? std::atoi(td_env) : 12;
+      for (; top_depth > 0; --top_depth) {  // the deepest whole levels that fit
+        uint32_t ns = 0;
+        if (!LayoutNodes(nodes, n_nodes, bvhs, n_bvhs, align, &remap, &ns, top_depth, &n_top)) {
+          top_depth = 0;
+          break;
+        }
+        if (td_env || ((2 * (size_t)n_top + 2 + 3) / 4) * srt::kNodeBlkF4 * sizeof(float4) <= budget) break;
+      }
+    }
+  }
+  bool laid = !(lay_env && lay_env[0] == '0') &&
+              LayoutNodes(nodes, n_nodes, bvhs, n_bvhs, align, &remap, &n_slots, top_depth, &n_top);
+  if (!laid) n_top = 0;
   // Triangle slots (LayoutTris) for every scene read through L2 (none of 1 MB fits the LDS copy):
   // fewer lines per leaf step (A/B on one box, kernel ms: C5 10 M 4096² 820 -> 773 with the IL leaf
   // step's own-record reads, 3 M 58.4 -> 56.5, 1 M 34.1 -> 32.6, torus knot 27.4 -> 27.4, Rubik
@@ -1914,6 +1979,8 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   c->sample_textures = sampled;
   c->bvhs_dirty = true;
   c->n_nodes = n_slots + srt::kNodePad;
+  c->top_f4 = n_top > 0 ? 2 * (int)n_top + 2 : 0;  // float4 of slots [0, n_top)
+  c->top_depth = n_top > 0 ? top_depth : 0;
   c->ref_or = laid ? 1u : 0u;
   c->n_tris = n_tslots;  // device records (slots)
   c->n_mats = n_mats;

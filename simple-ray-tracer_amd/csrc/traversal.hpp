@@ -651,21 +651,38 @@ __device__ __forceinline__ void trav_fused(const KParams& kp, const Lane& ln, Co
     // leaf: kLeafTris = 2 records (6 float4; kTriPad zero records keep them in
     // bounds); internal: the pair (4 float4) and, on the spine, the next pair
     static_assert(kLeafTris == 2, "trav_fused loads two triangle records");
-    const float4* p = at_leaf ? kp.tris + 3 * (size_t)t.ref : kp.nodes + (2 * ref0 + 2);
-    // (a one-triangle leaf still reads two records here: reading its own record twice, as
-    // trav_leaf does, measured 1% slower on the torus knot and within 0.5% elsewhere)
+    const uint32_t pi = 2 * ref0 + 2;
+    const float4* p = at_leaf ? kp.tris + 3 * (size_t)t.ref : kp.nodes + pi;
     float4 x[8];
-    x[0] = p[0];
-    x[1] = p[1];
-    x[2] = p[2];
-    x[3] = p[3];
-    if (at_leaf | spine) {
-      x[4] = p[4];
-      x[5] = p[5];
-    }
-    if (spine) {
-      x[6] = p[6];
-      x[7] = p[7];
+    // an internal step whose pair (and spine pair) lie in the top levels' region reads them from the
+    // block's LDS copy (padded pair blocks: the spine pair is the next block), off the vector-memory pipeline
+    if (at_int && pi + (spine ? 8u : 4u) <= (uint32_t)kp.top_f4) {
+      const uint32_t b = (uint32_t)kp.top_lds_f4 + (pi >> 2) * kNodeBlkF4;
+      x[0] = g_smem[b];
+      x[1] = g_smem[b + 1];
+      x[2] = g_smem[b + 2];
+      x[3] = g_smem[b + 3];
+      if (spine) {
+        x[4] = g_smem[b + kNodeBlkF4];
+        x[5] = g_smem[b + kNodeBlkF4 + 1];
+        x[6] = g_smem[b + kNodeBlkF4 + 2];
+        x[7] = g_smem[b + kNodeBlkF4 + 3];
+      }
+    } else {
+      // (a one-triangle leaf still reads two records here: reading its own record twice, as
+      // trav_leaf does, measured 1% slower on the torus knot and within 0.5% elsewhere)
+      x[0] = p[0];
+      x[1] = p[1];
+      x[2] = p[2];
+      x[3] = p[3];
+      if (at_leaf | spine) {
+        x[4] = p[4];
+        x[5] = p[5];
+      }
+      if (spine) {
+        x[6] = p[6];
+        x[7] = p[7];
+      }
     }
     if (at_int)
       trav_internal_x<COUNT, false, PACK, RING>(kp, ln, c, t, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], spine);

@@ -278,6 +278,36 @@ def test_triangle_slots(monkeypatch, tmp_path, rubik, env):
         assert (hits == hits_o).all() and bits_equal(t, t_o).all()
 
 
+@pytest.mark.parametrize("depth", [None, "3", "1", "0"])
+def test_top_levels_in_lds(monkeypatch, depth):
+    """The fused global-scene instance's LDS copy of the tree's top levels (pathtrace.hip LayoutNodes lays
+    their pairs out first; traversal.hpp trav_fused reads them from LDS): as deep as fits by default, or
+    SRT_TOP_DEPTH levels, or none; one and two BVHs (a moved second model) render the oracle's frame, and
+    the timed (fused) instance equals the counting one bit for bit (gpu_render)."""
+    if depth is not None:
+        monkeypatch.setenv("SRT_TOP_DEPTH", depth)
+    soup = R.make_setup(48, 40, show_model=True, models=[R.synthetic_model(30000, seed=3)])
+    r = R.Renderer(soup)
+    try:
+        want = {None: None, "3": 3, "1": 1, "0": 0}[depth]
+        got = r.compute.GetInt("scene.top_depth")
+        assert r.compute.GetInt("scene.fused") == 1
+        assert got == want if want is not None else got >= 6
+        r.render(1)
+        r.finish()
+        top_f4 = r.compute.GetInt("launch.top_f4")
+        assert top_f4 == r.compute.GetInt("scene.top_f4") and (top_f4 > 0) == (got > 0)
+    finally:
+        r.close()
+    assert_parity(soup, 2)
+    two = R.make_setup(40, 32, show_model=True, models=[R.synthetic_model(20000, seed=4),
+                                                        R.synthetic_model(5000, seed=6)])
+    frame = np.eye(4, dtype=np.float32)
+    frame[3, :3] = (1.5, -2.0, 0.5)
+    two.scene.bvhs[1]["frame"] = frame.reshape(16)
+    assert_parity(two, 2)
+
+
 @pytest.mark.parametrize("case", ["overlap", "shared"])
 def test_triangle_slots_unusual_leaves(case):
     """LayoutTris on leaf ranges no reference-built tree has: a leaf grown by one triangle into the next
