@@ -5,7 +5,7 @@ L2 would then serve one strip's rays.)  Renders the 8 row-band shares of a 1920x
 other on one GPU, as 2-row bands dealt round robin (every share spans the frame) and as 135-row bands (each
 share one contiguous strip), and prints the rays per kernel time of each split.
 
-  python tools/strip_probe.py [scene: torusknot|airplane_knot|synthetic] [spp]
+  python tools/strip_probe.py [scene: torusknot|airplane_knot|synthetic] [spp] [band rows, comma-separated: 2,135]
 """
 import pathlib
 import sys
@@ -22,7 +22,8 @@ def main():
     scene = sys.argv[1] if len(sys.argv) > 1 else "torusknot"
     spp = int(sys.argv[2]) if len(sys.argv) > 2 else 16
     setup, wl = bench.build_setup(scene, 1920, 1080, spp, 5, 1_000_000)
-    for band in (2, 135):
+    bands = [int(b) for b in sys.argv[3].split(",")] if len(sys.argv) > 3 else [2, 135]
+    for band in bands:
         rays = ms = 0.0
         for rank in range(8):
             r = R.Renderer(setup, rank=rank, nranks=8, band_rows=band)
