@@ -614,6 +614,10 @@ def parallelism(args, mode, world, run) -> str:
 
 def main(argv=None):
     args = parse(argv)
+    # 8 hardware queues per process (HIP's default is 4): torch's stream, the context's, its two pipeline slots'
+    # and, under torchrun, RCCL's then each get their own queue, so no gather queues behind a sample launch
+    # (measured neutral at N = 1: profiles/r05_experiments/pipeline_slots_queues.txt); set before HIP starts
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     import torch
     import torch.distributed as dist
 
