@@ -137,6 +137,9 @@ struct srt_context {
   // unpipelined launches, and one per pipeline slot), split equally: 21 GiB each with the 2 default slots
   size_t lbuf_total = (size_t)64 << 30;
   int tail_claims = 16;  // SRT_TAIL_CLAIMS: claims per wave before the end from which claims take one batch
+  int tail_claims_gw5 = 8;  // the untextured fused 5-wave instance's (torus knot +1.4% against 16 with two slots;
+                            // the textured Airplane material loses 0.6% and keeps 16;
+                            // profiles/r05_experiments/tail_window_overlap.txt); SRT_TAIL_CLAIMS sets it too
   int tail_claims_sph = 1;  // the sphere launch's (C2, 8 per claim: tail 16 6.20 ms, 1 3.17 ms; its batches
                             // are cheap, the counter's atomic rate bounds it); SRT_TAIL_CLAIMS sets both
   int trav_frac16 = 9;                 // SRT_TRAV_FRAC16 (measured best on Rubik 1080p with the 16-sub-step pattern)
@@ -537,7 +540,8 @@ int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
      // in round 1: 2 -> 16 halves the launch's tail)
     const long long waves = (long long)blocks * (BLOCK / 64);
     const long long n_batches = (long long)((kp.W + 7) >> 3) * ((kp.local_rows + 7) >> 3) * kp.nframes;
-    kp.tail_start = (int)std::max<long long>(0, n_batches - (long long)c->tail_claims * srt::kClaim * waves);
+    const int tail_claims = (FUSE && GW == 5 && !TEX) ? c->tail_claims_gw5 : c->tail_claims;
+    kp.tail_start = (int)std::max<long long>(0, n_batches - (long long)tail_claims * srt::kClaim * waves);
   }
   // the early-break threshold of the fused 4-wave instance (trees of 48-600 MB): 7, where the
   // latency-bound soups gain (1 M: 1,370 -> 1,413-1,418 Mrays/s; 3 M: 939 -> 971) and the 5-wave
@@ -1372,7 +1376,8 @@ int srt_create(int device, void* stream, srt_context** out) {
   if (const char* e = std::getenv("SRT_TREELET_DEPTH")) c->treelet_depth = std::max(0, std::min(srt::kTopStack - 1, std::atoi(e)));
   if (const char* e = std::getenv("SRT_PIPELINE")) c->pipe = std::max(1, std::min(8, std::atoi(e)));
   if (const char* e = std::getenv("SRT_PIPELINE_OVERLAP")) c->pipe_overlap = std::max(0, std::min(2, std::atoi(e)));
-  if (const char* e = std::getenv("SRT_TAIL_CLAIMS")) c->tail_claims = c->tail_claims_sph = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("SRT_TAIL_CLAIMS"))
+    c->tail_claims = c->tail_claims_sph = c->tail_claims_gw5 = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("SRT_TILE_ORDER")) c->tile_schedule = e[0] != '0';
   if (const char* e = std::getenv("SRT_TRAV_FRAC16")) c->trav_frac16 = std::max(0, std::min(16, std::atoi(e)));
   if (const char* e = std::getenv("SRT_TRAV_FRAC16_GLOBAL"))
