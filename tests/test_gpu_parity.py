@@ -498,6 +498,27 @@ def test_schedule_invariance(rubik, monkeypatch):
             monkeypatch.delenv(k)
 
 
+def test_global_schedule_invariance(monkeypatch):
+    """The same for the fused 5-wave global-scene instance, whose tail window is its own (8 claims per
+    wave, pathtrace.hip tail_claims_gw5): the default window, none, 16 claims and the whole launch give
+    the same bits, and the default renders the oracle's frame.  At this size every window covers the
+    whole launch but 0; the window's edge inside a launch is crossed by the at-size C3 stand-in tests
+    (test_gpu_configs.py), whose timed instance is this one."""
+    setup = R.make_setup(64, 48, show_model=True, models=[R.synthetic_model(30000, seed=3)])
+    r = R.Renderer(setup)
+    try:
+        assert r.compute.GetInt("scene.fused") == 1 and r.compute.GetInt("scene.global_waves") == 5
+    finally:
+        r.close()
+    a, o, _ = gpu_render(setup, 3)
+    for v in ("0", "16", "100000"):
+        monkeypatch.setenv("SRT_TAIL_CLAIMS", v)
+        b, p, _ = gpu_render(setup, 3)
+        assert bits_equal(a, b).all() and (o == p).all(), v
+    monkeypatch.delenv("SRT_TAIL_CLAIMS")
+    assert_parity(setup, 3)
+
+
 @pytest.mark.parametrize("nranks,band", [(2, 16), (3, 8), (2, 2), (3, 3), (8, 2), (5, 1)])
 def test_row_band_tiling_reassembles(rubik, nranks, band):
     import torch
