@@ -141,7 +141,7 @@ def algorithmic_bytes(st: dict) -> int:
 
 
 def cpu_baseline(setup, spp_first: int, target_s: float) -> dict:
-    """The oracle (scalar C restatement, OpenMP over rows) on this host, on a bounded sample of the workload:
+    """The oracle (scalar C restatement, OpenMP over row pieces) on this host, on a bounded sample of the workload:
     every 8th row of the frame, full width, consecutive frames of the same progressive sequence."""
     from oracle import pyoracle as O
 
@@ -166,7 +166,7 @@ def cpu_baseline(setup, spp_first: int, target_s: float) -> dict:
     rays = st["rays"] + st2["rays"]
     secs = (t1 - t0) + (t3 - t2)
     return {"value": rays / secs / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"oracle (gcc -O2 -mfma -ffp-contract=off: hardware FMA, OpenMP over rows) on {len(rows)} rows "
+            "sample": f"oracle (gcc -O2 -mfma -ffp-contract=off: hardware FMA, OpenMP over 64-pixel row pieces) on {len(rows)} rows "
                       f"(every 8th) x {s.width} px x {frames + 1} frames of the same workload ({rays} rays, "
                       f"{secs:.1f} s)"}
 

@@ -958,12 +958,16 @@ void oracle_render_rows(const OrScene* s, const OrFrame* f, int frame_first, int
   #pragma omp parallel num_threads(threads)
   {
     OrStats loc; memset(&loc, 0, sizeof loc);
+    /* pixels are independent and only each pixel's frames are ordered, so a row is split into
+     * 64-pixel pieces that run their frames in order: a few rows at many frames use every thread */
+    const int nxc = (f->width + 63) / 64;
     #pragma omp for schedule(dynamic, 1)
-    for (int r = 0; r < nrows; ++r) {
+    for (int it = 0; it < nrows * nxc; ++it) {
+      const int r = it / nxc, x0 = (it % nxc) * 64, x1 = x0 + 64 < f->width ? x0 + 64 : f->width;
       for (int k = 0; k < nframes; ++k) {
         OrFrame fk = *f; fk.accum_frames = frame_first + k; fk.reset = 0;
         Cam cam = get_camera(&fk);
-        for (int x = 0; x < f->width; ++x) invocation(s, &fk, &cam, x, rows[r], accum, out, &loc);
+        for (int x = x0; x < x1; ++x) invocation(s, &fk, &cam, x, rows[r], accum, out, &loc);
       }
     }
     #pragma omp critical
