@@ -20,12 +20,16 @@ N > 1 runs two ways, with the same kernels and the same exchange:
   torchrun --nproc-per-node N bench.py --gpus N
                                one process per GPU, torch.distributed over RCCL.
 
-Two more legs time the real-mesh path (scenes too large for the LDS scene copy,
-traversed from HBM/L2), each under "legs" with its own roofline; `value` is the
-main leg:
-  global_scene  a synthetic 1 M-triangle soup (SURVEY.md 8d generator), 1920x1080 @16 spp;
-  surface_mesh  a closed 262k-triangle surface (torus-knot tube, the stand-in for a
-                mesh such as the absent Airplane OBJ), 1920x1080 @64 spp.
+Three more legs time the real-mesh path (scenes too large for the LDS scene copy,
+traversed from HBM/L2), each under "legs" with its own roofline and ray mix; `value`
+is the main leg:
+  global_scene        a synthetic 1 M-triangle soup (SURVEY.md 8d generator), 1920x1080 @16 spp;
+  surface_mesh        a closed 262k-triangle surface (torus-knot tube wound outward, as an
+                      exported mesh is, so paths bounce off it), 1920x1080 @64 spp;
+  airplane_materials  C3's regime: the knot carrying the Airplane's six textured materials,
+                      sampled at each hit's uv, at C3's 1920x1080 @256 spp.  The absent Airplane
+                      OBJ would run in this mode (no real mesh fits the LDS copy), so the line
+                      repeats this leg at top level as `c3_regime`, beside the Rubik `value`.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -107,7 +111,8 @@ def parse(argv=None):
     # 26-ms leg would still show; the metric's 10 steps take 1.5 s)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default="rubik", choices=("rubik", "spheres", "synthetic", "torusknot", "airplane_knot"))
+    ap.add_argument("--scene", default="rubik",
+                    choices=("rubik", "spheres", "synthetic", "torusknot", "airplane_knot", "first_hit_knot"))
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=256)
@@ -122,7 +127,8 @@ def parse(argv=None):
     ap.add_argument("--no-surface-leg", action="store_true", help="skip the 262k-triangle surface-mesh leg")
     ap.add_argument("--surface-spp", type=int, default=64)
     ap.add_argument("--no-airplane-leg", action="store_true",
-                    help="skip the surface mesh carrying the Airplane's textured materials (C3's material path)")
+                    help="skip the surface mesh carrying the Airplane's textured materials (C3's regime)")
+    ap.add_argument("--airplane-spp", type=int, default=256, help="the Airplane-material leg's spp (C3's 256)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (multi-rank tests on one GPU)")
     ap.add_argument("--group", action="store_true",
@@ -299,9 +305,12 @@ def build_setup(scene: str, W: int, H: int, spp: int, max_depth: int, synthetic_
     elif scene == "synthetic":
         models = [R.synthetic_model(synthetic_tris)]
         show_model, wl = True, f"synthetic{synthetic_tris}_{W}x{H}_{spp}spp"
-    elif scene == "torusknot":
+    elif scene == "torusknot":  # outward faces, framed at render.SURFACE_KNOT_SCALE
         models = [R.torus_knot_model()]
-        show_model, wl = True, f"torusknot262144_{W}x{H}_{spp}spp"
+        show_model, wl = True, f"torusknot262144out_{W}x{H}_{spp}spp"
+    elif scene == "first_hit_knot":  # rounds 2-5's surface leg: inward faces, no path bounces
+        models = [R.first_hit_only_knot_model()]
+        show_model, wl = True, f"torusknot262144in_{W}x{H}_{spp}spp"
     elif scene == "airplane_knot":
         models = [airplane_knot_model()]
         show_model, wl = True, f"torusknot262144_airplane_materials_{W}x{H}_{spp}spp"
@@ -598,6 +607,13 @@ def timed_kernel(c, scene: str) -> str:
             f"{', textures sampled per hit' if tex else ''})")
 
 
+def ray_kinds(st: dict) -> dict:
+    """The counted rays by kind (srt_ray_kinds): camera (one per sample), shadow, bounce, and the bounce share."""
+    cam, sh = int(st["samples"]), int(st.get("shadow_rays", 0))
+    b = int(st["rays"]) - cam - sh
+    return {"camera": cam, "shadow": sh, "bounce": b, "bounce_share": round(b / max(int(st["rays"]), 1), 4)}
+
+
 def run_compute(run):
     return run.grp.parts[0].compute if isinstance(run, GroupRun) else run.c
 
@@ -614,10 +630,8 @@ def parallelism(args, mode, world, run) -> str:
 
 def main(argv=None):
     args = parse(argv)
-    # 8 hardware queues per process (HIP's default is 4): torch's stream, the context's, its two pipeline slots'
-    # and, under torchrun, RCCL's then each get their own queue, so no gather queues behind a sample launch
-    # (measured neutral at N = 1: profiles/r05_experiments/pipeline_slots_queues.txt); set before HIP starts
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    # (the box's default of 4 hardware queues per process, which the two pipeline slots are sized for: torch's
+    # stream, the context's and the two slots' each get one; profiles/r05_experiments/pipeline_slots_queues.txt)
     import torch
     import torch.distributed as dist
 
@@ -659,13 +673,13 @@ def main(argv=None):
     par = parallelism(args, mode, world, run)
     table = rank_table(per_ctx, run.rank_stats() if mode == "group" else [st], args, mode, world, dev)
     run.close()
-    global_main = args.scene in ("synthetic", "torusknot", "airplane_knot")
+    global_main = args.scene in ("synthetic", "torusknot", "airplane_knot", "first_hit_knot")
 
     legs = []
     for leg, enabled, scene, lw, lh, lspp, ntri in (
             ("global_scene", not args.no_global_leg, "synthetic", 1920, 1080, args.global_spp, args.global_tris),
             ("surface_mesh", not args.no_surface_leg, "torusknot", 1920, 1080, args.surface_spp, 0),
-            ("airplane_materials", not args.no_airplane_leg, "airplane_knot", 1920, 1080, args.surface_spp, 0)):
+            ("airplane_materials", not args.no_airplane_leg, "airplane_knot", 1920, 1080, args.airplane_spp, 0)):
         if not enabled:
             continue
         lsetup, lname = build_setup(scene, lw, lh, lspp, 5, ntri)
@@ -676,8 +690,9 @@ def main(argv=None):
         l_run.close()
         if rank == 0:
             desc = (f"synthetic {ntri} triangles (SURVEY 8d generator)" if scene == "synthetic" else
-                    "torus-knot tube, 262144 triangles (closed surface mesh; srt_amd.render.torus_knot_triangles), "
-                    "model camera and lights" if scene == "torusknot" else
+                    "torus-knot tube, 262144 triangles wound outward so paths bounce (closed surface mesh; "
+                    "srt_amd.render.torus_knot_triangles at SURFACE_KNOT_SCALE), model camera and lights"
+                    if scene == "torusknot" else
                     "the torus-knot tube with outward faces carrying the Airplane's six .mtl materials and diffuse "
                     "PNGs, textures sampled at each hit's uv (C3's material path; bench.airplane_knot_model)")
             l_ranks = per_rank_lines(l_table, lname, l_kname, True)
@@ -685,6 +700,7 @@ def main(argv=None):
                 "leg": leg, "workload": lname, "value": round(l_rays * args.steps / l_el / 1e6, 3),
                 "unit": "Mrays/s", "ms_per_step": round(l_el * 1e3 / args.steps, 3),
                 "config": {"scene": desc, "width": lw, "height": lh, "spp": lspp, "max_depth": 5},
+                "rays_per_step": int(l_rays), "ray_kinds": ray_kinds(l_st),
                 "kernel_ms_per_rank": [r["kernel_ms"] for r in l_ranks],
                 "exchange_ms_per_rank": [r["exchange_ms"] for r in l_ranks],
                 "roofline": max(l_ranks, key=lambda r: r["kernel_ms"])["roofline"],
@@ -718,6 +734,7 @@ def main(argv=None):
             "frame_ms": round(ms_per_step / spp, 4),
             "msamples_per_s": round(W * H * spp * args.steps / elapsed_s / 1e6, 3),
             "rays_per_step": int(total_rays),
+            "ray_kinds": ray_kinds(st),
             "code_hash": code_hash(),
             # sample-kernel throughput time per step of every rank (launches overlap their predecessor's
             # drain: each counts from its start or the previous launch's end to its end, srt_kernel_time),
@@ -730,6 +747,14 @@ def main(argv=None):
             "per_rank": ranks if world > 1 else None,
             "legs": legs,
         }
+        # C3's regime (BASELINE metric: the Airplane OBJ at 1920x1080 @256 spp): the absent mesh would run in
+        # global-scene mode, measured here on the surface carrying the Airplane's textured materials at C3's spp
+        c3 = next((l for l in legs if l["leg"] == "airplane_materials"), None)
+        line["c3_regime"] = None if c3 is None else {
+            "workload": c3["workload"], "value": c3["value"], "unit": "Mrays/s", "ms_per_step": c3["ms_per_step"],
+            "spp": c3["config"]["spp"], "ray_kinds": c3["ray_kinds"], "roofline": c3["roofline"],
+            "note": "the Airplane OBJ is absent (.MISSING_LARGE_BLOBS); any real mesh exceeds the LDS scene copy "
+                    "and runs this global-scene instance, so this is C3's regime; `value` stays the Rubik stand-in"}
         if group_info is not None:
             line["group"] = group_info
         elif mode == "dist":

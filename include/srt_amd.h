@@ -122,6 +122,10 @@ int srt_finish(srt_context* ctx);
  * uniform at frame_first + nframes - 1, as the last dispatch would. */
 int srt_render_frames(srt_context* ctx, int frame_first, int nframes, int write_output, int count);
 int srt_get_stats(srt_context* ctx, srt_stats* out);
+/* The counted rays by kind, of the same counting launches as srt_get_stats: [0] camera rays (one per
+ * path sample, GetRay), [1] shadow rays (CheckLightOccluded, raytrace_compute.glsl:167-176), [2] bounce
+ * rays (SampleIndirectNew's next ray, :224-290); they sum to srt_stats.rays. */
+int srt_ray_kinds(srt_context* ctx, uint64_t kinds[3]);
 /* Device time of the path-tracing kernel launches of the last render call: the
  * union of each sample_kernel / sphere_kernel launch's span (its first wave's
  * start to its last wave's end on the GPU's 100 MHz real-time clock), plus HIP
@@ -329,6 +333,9 @@ typedef struct { float diffuse[3]; float specular[3]; float specular_ex; uint32_
 int srt_model_sizes(const srt_model* m, uint32_t sizes[4]);
 int srt_model_copy(const srt_model* m, srt_host_bvh_node* nodes, srt_triangle* prims, srt_host_material* mats,
                    srt_vertex* verts);
+/* The BVH's primitive permutation (bvh.h:66-72: GetPrims()[i] is the loader's
+ * all_triangles[input_index[i]], model_loader.cpp:299-331); sizes[1] entries. */
+int srt_model_prim_order(const srt_model* m, uint32_t* input_index);
 
 /* Flatten models exactly as UploadModelDataToGPU does (index rebasing). */
 int srt_scene_build(const srt_model* const* models, uint32_t n_models, srt_scene** out);
@@ -337,6 +344,11 @@ int srt_scene_free(srt_scene* s);
 int srt_scene_sizes(const srt_scene* s, uint32_t sizes[5]);
 int srt_scene_copy(const srt_scene* s, srt_bvh_record* bvhs, srt_bvh_node* nodes, srt_material_obj* mats,
                    float* tex_albedo, srt_triangle* tris, srt_vertex* verts);
+/* Loader order of the flattened triangles: triangle i (the index srt_trace_closest
+ * returns) is input triangle input_index[i] of the models' concatenated loader
+ * order (each model's offset + srt_model_prim_order); sizes[3] entries.  The
+ * reference's ray KAT (BVH_intergration_tests.cpp:94) is stated in that order. */
+int srt_scene_tri_order(const srt_scene* s, uint32_t* input_index);
 /* Textures of the scene's use_texture materials (material handle = index);
  * sample_textures = 1 when a model was loaded with SRT_LOAD_TEXCOORDS. */
 int srt_scene_texture_count(const srt_scene* s, uint32_t* n, int* sample_textures);

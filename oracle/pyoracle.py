@@ -53,7 +53,8 @@ class OrFrame(C.Structure):
 
 class OrStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("rays", "nodes", "tris", "rng_u", "rng_sq", "light_reads",
-                                           "mat_reads", "samples", "stack_overflow", "max_stack")]
+                                           "mat_reads", "samples", "stack_overflow", "max_stack",
+                                           "shadow_rays")]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}

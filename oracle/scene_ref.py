@@ -299,7 +299,9 @@ def _vmax(a, b):  # glm::max: x < y ? y : x
     return tuple(b[i] if a[i] < b[i] else a[i] for i in range(3))
 
 
-def build_bvh(packed, tris):
+def build_bvh(packed, tris, with_order=False):
+    """bvh.h:40-75.  Returns (nodes, prims, depth), and with ``with_order`` also the primitive permutation
+    ``idx`` of bvh.h:66-72 (prims[i] = tris[idx[i]]: BVH order -> the loader's order)."""
     n = len(tris)
     centers, bmin, bmax = [], [], []
     for t in tris:
@@ -359,6 +361,8 @@ def build_bvh(packed, tris):
     subdivide(0, 0)
     nodes = nodes[:state["next"]]
     prims = [tris[i] for i in idx]
+    if with_order:
+        return nodes, prims, state["depth"], idx
     return nodes, prims, state["depth"]
 
 

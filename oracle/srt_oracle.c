@@ -558,6 +558,7 @@ static HitRecord check_hit(Ctx* c, v3 ro, v3 rd, float mn, float mx) {
 static int light_occluded(Ctx* c, v3 pos, const Light* L) {
   v3 dir = normalize3(sub(L->pos, pos));
   float mx = length3(sub(L->pos, pos));
+  c->st->shadow_rays++;
   HitRecord r = check_hit(c, pos, dir, 0.001f, mx);
   return r.hit;
 }
@@ -915,7 +916,7 @@ void oracle_dispatch(const OrScene* s, const OrFrame* f, float* accum, uint8_t* 
 static void stats_add(OrStats* a, const OrStats* b) {
   a->rays += b->rays; a->nodes += b->nodes; a->tris += b->tris; a->rng_u += b->rng_u;
   a->rng_sq += b->rng_sq; a->light_reads += b->light_reads; a->mat_reads += b->mat_reads;
-  a->samples += b->samples; a->stack_overflow += b->stack_overflow;
+  a->samples += b->samples; a->stack_overflow += b->stack_overflow; a->shadow_rays += b->shadow_rays;
   if (b->max_stack > a->max_stack) a->max_stack = b->max_stack;
 }
 

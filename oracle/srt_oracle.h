@@ -86,6 +86,7 @@ typedef struct {
   uint64_t samples;      /* path samples */
   uint64_t stack_overflow; /* traversals that would overflow stack[64] */
   uint64_t max_stack;    /* deepest stack seen */
+  uint64_t shadow_rays;  /* of `rays`: CheckLightOccluded's queries (raytrace_compute.glsl:167-176) */
 } OrStats;
 
 /* One glDispatchCompute of raytrace_compute.glsl over rows [y0, y1) and all

@@ -145,6 +145,14 @@ int srt_model_copy(const srt_model* mm, srt_host_bvh_node* nodes, srt_triangle* 
   return SRT_OK;
 }
 
+int srt_model_prim_order(const srt_model* mm, uint32_t* input_index) {
+  if (!mm || !mm->m || !input_index) return SRT_ERR_INVALID;
+  const srt::Model& m = *mm->m;
+  for (size_t i = 0; i < m.prims.size(); ++i)
+    input_index[i] = i < m.prim_input.size() ? m.prim_input[i] : (uint32_t)i;
+  return SRT_OK;
+}
+
 int srt_scene_build(const srt_model* const* models, uint32_t n_models, srt_scene** out) {
   if (!out || (n_models && !models)) return SRT_ERR_INVALID;
   std::vector<const srt::Model*> ms;
@@ -171,6 +179,12 @@ int srt_scene_sizes(const srt_scene* s, uint32_t sizes[5]) {
   sizes[2] = (uint32_t)s->s->mats.size();
   sizes[3] = (uint32_t)s->s->tris.size();
   sizes[4] = (uint32_t)s->s->verts.size();
+  return SRT_OK;
+}
+
+int srt_scene_tri_order(const srt_scene* s, uint32_t* input_index) {
+  if (!s || !input_index) return SRT_ERR_INVALID;
+  std::memcpy(input_index, s->s->tri_input.data(), s->s->tri_input.size() * sizeof(uint32_t));
   return SRT_OK;
 }
 

@@ -83,6 +83,7 @@ extern __shared__ __attribute__((aligned(16))) float4 g_smem[];
 
 enum { ST_RAYS = 0, ST_NODES, ST_TRIS, ST_RNGU, ST_RNGSQ, ST_LIGHTS, ST_MATS, ST_SAMPLES, ST_OVERFLOW, ST_MAXSTACK,
        ST_BOUNCECAP,  // paths cut at the bounce cap (KParams::bounce_cap)
+       ST_SHADOW,     // shadow rays among ST_RAYS (CheckLightOccluded, raytrace_compute.glsl:167-176)
        ST_N, ST_CYC_REFILL = ST_N, ST_CYC_TRAV, ST_CYC_SHADE, ST_CYC_ITERS,
        // lane occupancy of the traversal loop (summed popcounts per iteration) and of shading
        ST_DBG_TITERS, ST_DBG_WORK, ST_DBG_TRAV, ST_DBG_LEAF, ST_DBG_INT, ST_DBG_SHADE,

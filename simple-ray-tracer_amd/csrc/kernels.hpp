@@ -356,6 +356,7 @@ __device__ __forceinline__ void sample_body(const KParams& kp) {
     tr.active = true;
     tr.start = false;
     bump<COUNT>(c, ST_RAYS);
+    bump<COUNT>(c, ST_SHADOW, shadow_phase ? 1u : 0u);
     if constexpr (!SPH) {
       trav_begin_bvh<COUNT, LDSM>(kp, c, tr, ro, rd);
       if (tr.cnt == kNoneCnt) {  // root box missed: next BVH, or done

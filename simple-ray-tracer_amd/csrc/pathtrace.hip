@@ -182,6 +182,7 @@ struct srt_context {
   unsigned long long* d_stats = nullptr;
   unsigned long long* d_nan = nullptr;  // NaN path samples since the last srt_reset_stats
   srt_stats stats{};
+  uint64_t shadow_rays = 0;  // of stats.rays (srt_ray_kinds)
   // per-chunk HIP events around the sample kernel of the last render call
   std::vector<hipEvent_t> ev;
   struct Occupancy {
@@ -1121,6 +1122,7 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
     c->stats.stack_overflow += s[srt::ST_OVERFLOW];
     c->stats.bounce_cap += s[srt::ST_BOUNCECAP];
     c->stats.max_stack = std::max<uint64_t>(c->stats.max_stack, s[srt::ST_MAXSTACK]);
+    c->shadow_rays += s[srt::ST_SHADOW];
   }
   return SRT_OK;
 }
@@ -1704,9 +1706,18 @@ int srt_get_stats(srt_context* c, srt_stats* out) {
   return SRT_OK;
 }
 
+int srt_ray_kinds(srt_context* c, uint64_t kinds[3]) {
+  if (!c || !kinds) return SRT_ERR_INVALID;
+  kinds[0] = c->stats.samples;  // one camera ray per path sample
+  kinds[1] = c->shadow_rays;
+  kinds[2] = c->stats.rays - c->stats.samples - c->shadow_rays;
+  return SRT_OK;
+}
+
 int srt_reset_stats(srt_context* c) {
   if (!c) return SRT_ERR_INVALID;
   c->stats = srt_stats{};
+  c->shadow_rays = 0;
   HIP_OK(hipSetDevice(c->device));
   HIP_OK(hipMemsetAsync(c->d_nan, 0, sizeof(unsigned long long), c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));

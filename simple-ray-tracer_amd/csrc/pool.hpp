@@ -393,6 +393,7 @@ __device__ __forceinline__ void pool_trace(const KParams& kp, Pool& P, Counters&
       tr.active = true;
       tr.start = false;
       bump<COUNT>(c, ST_RAYS);
+      bump<COUNT>(c, ST_SHADOW, (pr.flags & kFlagShadow) ? 1u : 0u);
       trav_begin_bvh<COUNT, true>(kp, c, tr, pr.ro, pr.rd);
       if (tr.cnt == kNoneCnt) {  // root box missed: next BVH, or done
         if (kp.bvh_count > 1) tr.start = true, tr.bi = 1;

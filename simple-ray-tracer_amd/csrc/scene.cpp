@@ -256,6 +256,7 @@ class BvhBuilder {
       for (size_t i = c * chunk; i < std::min(n, (c + 1) * chunk); ++i) np[i] = m_->prims[idx_[i]];
     });
     m_->prims = std::move(np);
+    m_->prim_input = idx_;
     m_->nodes = std::move(nodes);
     m_->max_depth = max_depth;
     m_->leaves = leaves;
@@ -724,6 +725,8 @@ std::unique_ptr<Scene> FlattenModels(const std::vector<const Model*>& models, st
       g.material_idx = t.material_idx + model_mat_off;
       s->tris.push_back(g);
     }
+    for (size_t i = 0; i < m->prims.size(); ++i)
+      s->tri_input.push_back(local_tri_off + (i < m->prim_input.size() ? m->prim_input[i] : (uint32_t)i));
     tri_off += static_cast<uint32_t>(m->prims.size());
     for (const auto& n : m->nodes) {
       srt_bvh_node g;

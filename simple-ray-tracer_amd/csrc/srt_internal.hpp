@@ -64,6 +64,7 @@ struct Material {
 struct Model {
   std::vector<BVHNode> nodes;
   std::vector<Triangle> prims;         // BVH-ordered
+  std::vector<uint32_t> prim_input;    // prims[i] is the loader's triangle prim_input[i] (bvh.h:66-72)
   std::vector<Material> materials;
   std::vector<srt_vertex> vertices;    // PackedVertexData, 32 B
   std::vector<Texture> textures;       // one per distinct map_Kd file
@@ -80,6 +81,7 @@ struct Scene {
   std::vector<srt_material_obj> mats;
   std::vector<float> tex_albedo;       // 3 per material
   std::vector<srt_triangle> tris;
+  std::vector<uint32_t> tri_input;       // tris[i] in loader order: model offset + Model::prim_input
   std::vector<srt_vertex> verts;
   std::vector<Texture> textures;         // material handle = index
   bool sample_textures = false;          // some model carries real uvs

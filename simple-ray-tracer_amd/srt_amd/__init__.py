@@ -253,6 +253,14 @@ class Model:
         d["root_min"], d["root_max"] = mn, mx
         return d
 
+    def prim_order(self) -> np.ndarray:
+        """The BVH's primitive permutation (bvh.h:66-72): GetPrims()[i] is loader triangle ``out[i]``."""
+        sizes = np.zeros(4, np.uint32)
+        check(lib().srt_model_sizes(self._h, _ptr(sizes)), "srt_model_sizes")
+        out = np.zeros(sizes[1], np.uint32)
+        check(lib().srt_model_prim_order(self._h, _ptr(out)), "srt_model_prim_order")
+        return out
+
     def __del__(self):
         if getattr(self, "_h", None) and _lib._lib is not None:
             _lib._lib.srt_model_free(self._h)
@@ -309,6 +317,7 @@ class Scene:
     verts: np.ndarray
     textures: list = field(default_factory=list)  # (H, W, C) uint8 per texture handle
     sample_textures: bool = False                  # sample at the hit's uv instead of tex_albedo
+    tri_input: np.ndarray | None = None            # loader-order index of each triangle (srt_scene_tri_order)
 
     @classmethod
     def from_models(cls, models: Sequence[Model | None]) -> "Scene":
@@ -322,6 +331,8 @@ class Scene:
                     np.zeros((sizes[2], 3), np.float32), np.zeros(sizes[3], TRI_DTYPE), np.zeros(sizes[4], VERT_DTYPE))
             check(lib().srt_scene_copy(sh, _ptr(s.bvhs), _ptr(s.nodes), _ptr(s.mats), _ptr(s.tex_albedo),
                                        _ptr(s.tris), _ptr(s.verts)), "srt_scene_copy")
+            s.tri_input = np.zeros(sizes[3], np.uint32)
+            check(lib().srt_scene_tri_order(sh, _ptr(s.tri_input)), "srt_scene_tri_order")
             n, sample = C.c_uint32(), C.c_int()
             check(lib().srt_scene_texture_count(sh, C.byref(n), C.byref(sample)), "srt_scene_texture_count")
             for i in range(n.value):
@@ -515,9 +526,18 @@ class Compute:
               "render_frames")
 
     def stats(self) -> dict:
+        """srt_get_stats, plus "shadow_rays" (srt_ray_kinds' shadow count, as the oracle's stats name it)."""
         s = _lib.Stats()
         check(lib().srt_get_stats(self.ctx, C.byref(s)), "stats")
-        return s.as_dict()
+        d = s.as_dict()
+        d["shadow_rays"] = self.ray_kinds()["shadow"]
+        return d
+
+    def ray_kinds(self) -> dict:
+        """The counted rays by kind (srt_ray_kinds): camera, shadow and bounce rays; they sum to stats()["rays"]."""
+        k = np.zeros(3, np.uint64)
+        check(lib().srt_ray_kinds(self.ctx, _ptr(k)), "ray_kinds")
+        return {"camera": int(k[0]), "shadow": int(k[1]), "bounce": int(k[2])}
 
     def last_kernel_ms(self) -> float:
         """Device time of the sample-kernel launches of the last render (each launch's span on the GPU clock)."""

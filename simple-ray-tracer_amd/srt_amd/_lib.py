@@ -101,6 +101,7 @@ _SIGS = {
     "srt_finish": (C.c_int, [P]),
     "srt_render_frames": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int]),
     "srt_get_stats": (C.c_int, [P, C.POINTER(Stats)]),
+    "srt_ray_kinds": (C.c_int, [P, P]),
     "srt_last_kernel_ms": (C.c_int, [P, C.POINTER(C.c_float)]),
     "srt_kernel_time": (C.c_int, [P, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     "srt_reset_stats": (C.c_int, [P]),
@@ -154,10 +155,12 @@ _SIGS = {
     "srt_model_info": (C.c_int, [P, P, P, P]),
     "srt_model_sizes": (C.c_int, [P, P]),
     "srt_model_copy": (C.c_int, [P, P, P, P, P]),
+    "srt_model_prim_order": (C.c_int, [P, P]),
     "srt_scene_build": (C.c_int, [P, C.c_uint32, C.POINTER(P)]),
     "srt_scene_free": (C.c_int, [P]),
     "srt_scene_sizes": (C.c_int, [P, P]),
     "srt_scene_copy": (C.c_int, [P, P, P, P, P, P, P]),
+    "srt_scene_tri_order": (C.c_int, [P, P]),
     "srt_scene_texture_count": (C.c_int, [P, C.POINTER(C.c_uint32), C.POINTER(C.c_int)]),
     "srt_scene_texture": (C.c_int, [P, C.c_uint32, C.POINTER(Texture)]),
     "srt_upload_scene_obj": (C.c_int, [P, P]),

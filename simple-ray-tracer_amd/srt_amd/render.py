@@ -297,8 +297,9 @@ def synthetic_triangles(n_tris: int, seed: int = 0x5EED2025) -> np.ndarray:
     return tri.reshape(n_tris, 9)
 
 
-def torus_knot_grid(n_u: int = 512, n_v: int = 256, p: int = 2, q: int = 3) -> np.ndarray:
-    """The (n_u, n_v, 3) float64 vertex grid of torus_knot_triangles' tube (u along the knot, v around it)."""
+def torus_knot_grid(n_u: int = 512, n_v: int = 256, p: int = 2, q: int = 3, scale: float = 1.0) -> np.ndarray:
+    """The (n_u, n_v, 3) float64 vertex grid of torus_knot_triangles' tube (u along the knot, v around it),
+    `scale` times the unit size about the centre (0, 9, 0)."""
     u = np.arange(n_u, dtype=np.float64) * (2.0 * np.pi / n_u)
     v = np.arange(n_v, dtype=np.float64) * (2.0 * np.pi / n_v)
 
@@ -314,19 +315,39 @@ def torus_knot_grid(n_u: int = 512, n_v: int = 256, p: int = 2, q: int = 3) -> n
     n1 /= np.linalg.norm(n1, axis=-1, keepdims=True)
     n2 = np.cross(tang, n1)
     rad = 2.4
-    return c[:, None, :] + rad * (np.cos(v)[None, :, None] * n1[:, None, :] + np.sin(v)[None, :, None] * n2[:, None, :])
+    g = c[:, None, :] + rad * (np.cos(v)[None, :, None] * n1[:, None, :] + np.sin(v)[None, :, None] * n2[:, None, :])
+    if scale != 1.0:
+        ctr = np.array([0.0, 9.0, 0.0])
+        g = ctr + scale * (g - ctr)
+    return g
 
 
-def torus_knot_triangles(n_u: int = 512, n_v: int = 256, p: int = 2, q: int = 3) -> np.ndarray:
+# The surface-mesh stand-in's size: the unit knot covers 22% of the model camera's frame, so 81% of its rays
+# would be camera and shadow rays; at 1.5 it fills about half of it, as a framed model does, and 29% of the
+# counted rays are bounce rays (oracle, 192x108 @ 4 spp).  The Airplane-material knot keeps the unit size.
+SURFACE_KNOT_SCALE = 1.5
+
+
+def torus_knot_triangles(n_u: int = 512, n_v: int = 256, p: int = 2, q: int = 3, outward: bool = True,
+                         scale: float = 1.0) -> np.ndarray:
     """A closed surface mesh for the global-scene path (the Airplane OBJ is absent): a (p, q) torus-knot tube,
     2 * n_u * n_v triangles, centred at (0, 9, 0) in the Rubik's extent (~18 units across) so the model camera
-    and lights of src/main.cpp frame it.  Deterministic (float64 numpy, rounded once to float32)."""
-    pts = torus_knot_grid(n_u, n_v, p, q)
+    and lights of src/main.cpp frame it.  Deterministic (float64 numpy, rounded once to float32).
+
+    `outward` (the default): faces wound so that the geometric normal normalize(cross(e1, e2)), which the shader
+    uses as is (ray_intersects.glsl:90, raytrace_compute.glsl:157: not face-forwarded), points out of the tube,
+    as an exported model's does, so paths bounce off it.  `outward=False` is the inward winding of rounds 2-5
+    (first_hit_only_knot_model): SampleIndirectNew rejects every bounce there (dot(N, V) <= 0, brdf.glsl:242),
+    so a path ends after its first hit's shadow ray."""
+    pts = torus_knot_grid(n_u, n_v, p, q, scale)
     i0 = np.arange(n_u)[:, None]
     j0 = np.arange(n_v)[None, :]
     i1, j1 = (i0 + 1) % n_u, (j0 + 1) % n_v
     a, b, cc, d = pts[i0, j0], pts[i1, j0], pts[i1, j1], pts[i0, j1]
-    tri = np.stack([np.stack([a, b, cc], axis=-2), np.stack([a, cc, d], axis=-2)], axis=2)  # (n_u, n_v, 2, 3, 3)
+    if outward:
+        tri = np.stack([np.stack([a, cc, b], axis=-2), np.stack([a, d, cc], axis=-2)], axis=2)
+    else:
+        tri = np.stack([np.stack([a, b, cc], axis=-2), np.stack([a, cc, d], axis=-2)], axis=2)  # (n_u, n_v, 2, 3, 3)
     return tri.reshape(-1, 9).astype(np.float32)
 
 
@@ -367,8 +388,18 @@ def write_textured_torus_knot_obj(path: str | pathlib.Path, mtllib: str, materia
     return path
 
 
-def torus_knot_model(n_u: int = 512, n_v: int = 256) -> Model:
-    return model_from_triangles(torus_knot_triangles(n_u, n_v), kd=(0.8, 0.6, 0.3), ks=(0.5, 0.5, 0.5), ns=40.0)
+def torus_knot_model(n_u: int = 512, n_v: int = 256, outward: bool = True,
+                     scale: float = SURFACE_KNOT_SCALE) -> Model:
+    """The surface-mesh stand-in for C3's regime (bench.py's surface_mesh leg): the outward-wound knot at
+    SURFACE_KNOT_SCALE, paths bouncing off it."""
+    return model_from_triangles(torus_knot_triangles(n_u, n_v, outward=outward, scale=scale), kd=(0.8, 0.6, 0.3),
+                                ks=(0.5, 0.5, 0.5), ns=40.0)
+
+
+def first_hit_only_knot_model(n_u: int = 512, n_v: int = 256) -> Model:
+    """The surface-mesh leg of rounds 2-5: the unit-size knot wound inward, so no path bounces
+    (torus_knot_triangles(outward=False)); kept for comparisons only."""
+    return torus_knot_model(n_u, n_v, outward=False, scale=1.0)
 
 
 def synthetic_model(n_tris: int, seed: int = 0x5EED2025) -> Model:

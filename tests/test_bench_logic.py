@@ -65,8 +65,8 @@ def test_counters_of_other_code_give_no_roof(monkeypatch):
 
 def test_committed_counters_are_for_the_sources():
     """profiles/counters.json must hold counters of the code the sources build: every workload's code_hash
-    equals the hash the product build stamps (Makefile `hash`: kernel sources, srt_amd.h and the hipcc
-    flags).  A kernel edit without a re-capture (tools/gpu_round_profiles.sh) would leave the bench line
+    equals the hash the product build stamps (Makefile `hash`: the preprocessed device translation unit and
+    the hipcc flags).  A kernel edit without a re-capture (tools/gpu_round_profiles.sh) would leave the bench line
     without roofs."""
     import json
     import pathlib
@@ -88,6 +88,36 @@ def test_valu_issue_against_the_calibrated_rate(stub):
     cal = rf["valu_issue_calibrated"]
     assert cal["waves_per_simd"] == 4 and cal["peak"] < bench.VALU_PEAK_GIPS
     assert cal["frac"] == pytest.approx(rf["fractions"]["valu_issue"] * bench.VALU_PEAK_GIPS / cal["peak"], rel=1e-3)
-    g = bench.roofline("torusknot262144_1920x1080_64spp", 26.2, 10,
+    g = bench.roofline("torusknot262144out_1920x1080_64spp", 26.2, 10,
                        "srt::sample_kernel<...> (global-scene mode, fused sub-steps, 5 waves per SIMD)", global_mode=True)
     assert g["valu_issue_calibrated"]["waves_per_simd"] == 5 and "8 waves" in g["valu_issue_calibrated"]["basis"]
+
+
+def test_code_hash_ignores_prose_but_not_code(tmp_path):
+    """the code hash is the preprocessed translation unit of pathtrace.hip (comments and
+    blank lines gone) plus the hipcc flags, so a comment edit in include/srt_amd.h or a kernel header leaves it
+    alone, while a code edit changes it (and counters of other code are then rejected, test above)."""
+    import pathlib
+    import shutil
+    import subprocess
+
+    root = pathlib.Path(__file__).resolve().parent.parent
+    pkg = tmp_path / "pkg"
+    shutil.copytree(root / "simple-ray-tracer_amd" / "csrc", pkg / "csrc")
+    shutil.copy(root / "simple-ray-tracer_amd" / "Makefile", pkg / "Makefile")
+    shutil.copytree(root / "include", tmp_path / "include")
+
+    def h():
+        return subprocess.run(["make", "-s", "-C", str(pkg), "hash"], check=True, capture_output=True,
+                              text=True).stdout.strip()
+
+    base = h()
+    assert len(base) == 16 and base != "pp-failed"
+    hdr = tmp_path / "include" / "srt_amd.h"
+    hdr.write_text(hdr.read_text().replace("/* Closest-hit query:", "/* Closest-hit query (reworded):\n\n *"))
+    trav = pkg / "csrc" / "traversal.hpp"
+    trav.write_text("// a new comment line\n" + trav.read_text())
+    assert h() == base
+    k = pkg / "csrc" / "kernels.hpp"
+    k.write_text(k.read_text().replace("mk(0.05f, 0.05f, 0.05f)", "mk(0.05f, 0.05f, 0.06f)", 1))
+    assert h() != base

@@ -236,17 +236,36 @@ def test_c3_standin_airplane_materials_textured_1080p_256spp(tmp_path):
 def test_c3_standin_surface_mesh_1080p_256spp():
     """C3's regime (the Airplane OBJ is absent: .MISSING_LARGE_BLOBS): a real surface mesh in global-scene
     mode at C3's frame and spp, 1920x1080 @ 256 spp -- the bench's surface-mesh scene (torus-knot tube,
-    262,144 triangles, model camera and lights) through the timed fused instance at 5 waves per SIMD, bit-equal
-    to the counting instance over the whole frame and to the oracle on rows spread across it."""
+    262,144 triangles wound outward as an exported model is, framed at SURFACE_KNOT_SCALE; model camera and
+    lights) through the timed fused instance at 5 waves per SIMD, bit-equal to the counting instance over the
+    whole frame and to the oracle on rows spread across it.  Paths bounce off it (the inward
+    knot of rounds 2-5 rejected every bounce at dot(N, V) <= 0, brdf.glsl:242): bounce rays are at least 20%
+    of the counted rays (srt_ray_kinds), and the oracle's rows see the same ray mix."""
     setup = R.make_setup(1920, 1080, show_model=True, models=[R.torus_knot_model()])
     assert timed_instance(setup) == "fused5"
     spp = 256
     a, o, st = gpu_render(setup, spp)
     assert st["samples"] == 1920 * 1080 * spp and st["stack_overflow"] == 0
+    bounce = st["rays"] - st["samples"] - st["shadow_rays"]
+    assert bounce >= 0.20 * st["rays"], (bounce, st)
     rows = spread_rows(1080, 12)
-    acc, out, _ = oracle_render(setup, spp, rows=rows)
+    acc, out, ost = oracle_render(setup, spp, rows=rows)
     assert_rows(a, o, acc, out, rows)
+    assert ost["rays"] - ost["samples"] - ost["shadow_rays"] >= 0.15 * ost["rays"]
     assert st["tris"] > st["samples"]  # (the mesh covers much of the frame: more triangle tests than samples)
+
+
+def test_first_hit_only_knot_never_bounces():
+    """The inward-wound knot the surface-mesh leg used in rounds 2-5 (render.first_hit_only_knot_model): every
+    bounce is rejected (dot(N, V) <= 0, brdf.glsl:242), so its rays are camera and shadow rays only; the outward
+    knot of the same grid bounces.  192x108 @ 4 spp, counting instance, against the oracle's counts."""
+    for model, bounces in ((R.first_hit_only_knot_model(), False), (R.torus_knot_model(scale=1.0), True)):
+        setup = R.make_setup(192, 108, show_model=True, models=[model])
+        _, _, st = gpu_render(setup, 4, timed=False)
+        _, _, ost = oracle_render(setup, 4)
+        assert (st["rays"], st["shadow_rays"]) == (ost["rays"], ost["shadow_rays"])
+        b = st["rays"] - st["samples"] - st["shadow_rays"]
+        assert (b > 0.1 * st["rays"]) if bounces else (b < 1e-3 * st["rays"]), (b, st)
 
 
 def _coincident_star(n=300, seed=5):

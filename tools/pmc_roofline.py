@@ -25,11 +25,11 @@ tag = sys.argv[sys.argv.index("--tag") + 1] if "--tag" in sys.argv else out_dir.
 only = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else None
 root = pathlib.Path(__file__).resolve().parent.parent
 
-AIRPLANE_LEG = "torusknot262144_airplane_materials_1920x1080_64spp"  # bench.py's texture-sampling leg
+AIRPLANE_LEG = "torusknot262144_airplane_materials_1920x1080_256spp"  # bench.py's texture-sampling leg (C3's spp)
 LEGS = {  # kernel instance -> the workloads bench.py runs on it, in launch order (one timed launch each)
     "void srt::sample_kernel<false, true, true, 1024, false, false, 4>": ["rubik_1920x1080_256spp"],
     "void srt::sample_kernel<false, false, true, 256, false, true, 4>": ["synthetic1000000_1920x1080_16spp"],
-    "void srt::sample_kernel<false, false, true, 256, false, true, 5>": ["torusknot262144_1920x1080_64spp"],
+    "void srt::sample_kernel<false, false, true, 256, false, true, 5>": ["torusknot262144out_1920x1080_64spp"],
     "void srt::sample_kernel<false, false, true, 256, true, true, 5>": [AIRPLANE_LEG],
 }
 
