@@ -155,12 +155,23 @@ int srt_set_tiling(srt_context* ctx, int rank, int nranks, int band_rows);
 int srt_local_rows(srt_context* ctx);
 /* The context's HIP device, and a uniform's current value (glGetUniformiv): the int / uint / bool
  * uniforms above by name; SRT_ERR_NOT_FOUND for other names.  Read-only names report what the
- * uploaded scene's size chose for global-scene mode's timed kernel: "scene.fused" (1: fused
- * sub-steps, 0: the IL pattern), "scene.global_waves" (waves per SIMD of the fused instance) and
- * "scene.tri_slots" (device triangle records: more than the scene's triangles when small leaves
- * are laid out line by line for a tree streamed from HBM); and of the last render call,
- * "launch.chunks" (its sample launches: one per sample-buffer chunk) and "launch.overlap" (1 when
- * its launches may start while the previous one drains, SRT_PIPELINE_OVERLAP). */
+ * uploaded scene's size chose for global-scene mode's timed kernel:
+ *   "scene.fused"        1: fused sub-steps, 0: the IL pattern;
+ *   "scene.global_waves" waves per SIMD of the fused instance;
+ *   "scene.tri_slots"    device triangle records (more than the scene's triangles when small leaves are
+ *                        laid out line by line for a tree streamed from HBM);
+ *   "scene.top_depth", "scene.top_f4"  levels and float4 of the tree's top region the fused instance
+ *                        copies into each block's LDS (0: none);
+ *   "scene.wavefront", "scene.wf_waves", "scene.treelets"  the opt-in wavefront mode's choices;
+ * and of the last render call:
+ *   "launch.chunks"      its sample launches (one per sample-buffer chunk);
+ *   "launch.overlap"     1 when its launches ran on the pipeline slots, each free to start while the
+ *                        previous one drains (SRT_PIPELINE_OVERLAP), 0 otherwise (counting, pool and
+ *                        wavefront launches run in series);
+ *   "launch.top_f4"      the top region its global-scene launch copied (0: none: the region did not fit
+ *                        beside the rings and the light and material records);
+ *   "launch.blocks_per_cu", "launch.block"  resident blocks per CU and lanes per block of its last
+ *                        sample launch. */
 int srt_device(srt_context* ctx);
 int srt_get_int(srt_context* ctx, const char* name, int* v);
 

@@ -64,7 +64,10 @@ __device__ __forceinline__ int lane_rank(unsigned long long mask, int lane) {
 // dwords spilled; 8-entry rings, 16 KiB per block) for trees small enough that
 // more rays in flight beat the spills (srt_upload_scene picks it by scene size).
 // (SRT_COOP builds keep 8-entry rings at either regime: the cooperative loads' stage takes the rest)
-__host__ __device__ constexpr int global_ring(int gw) { return (gw > 4 || SRT_COOP) ? 8 : kShortStack; }
+#ifndef SRT_RING_GW5
+#define SRT_RING_GW5 8
+#endif
+__host__ __device__ constexpr int global_ring(int gw) { return (gw > 4 || SRT_COOP) ? SRT_RING_GW5 : kShortStack; }
 // GetRayColor's loop body for a ray whose CheckHit hit (raytrace_compute.glsl:225-290): the
 // hit record, this bounce's draws, SampleLights, both shadow outcomes of the direct light
 // (q0: occluded, q1: visible), the BRDF choice, Russian roulette and the next direction.

@@ -31,6 +31,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include <zlib.h>
@@ -103,6 +104,8 @@ struct srt_context {
   bool fused = false;         // global-scene mode's fused sub-steps (set at upload: trees the Infinity Cache holds)
   int top_f4 = 0, top_depth = 0;  // the node array's top-level region (LayoutNodes) the fused instance copies to LDS
   int launch_top_f4 = 0;           // the region the last global-scene launch copied (0: none)
+  bool launch_overlap = false;     // the last render's sample launches ran piped and overlapped (launch.overlap)
+  int launch_per_cu = 0, launch_block = 0;  // resident blocks per CU and lanes per block of the last sample launch
   int global_waves = 4;       // the fused instance's waves per SIMD (set at upload: 5 for small trees)
   // lights
   std::vector<srt_light> h_lights;
@@ -495,6 +498,19 @@ constexpr size_t kLdsBytes = 160 * 1024;
 #define SRT_LDS_BLOCK 1024
 #endif
 constexpr int kLdsBlock = SRT_LDS_BLOCK;
+// Global-scene mode's block: 256 lanes, except the timed fused instance at 5 waves per SIMD, whose blocks
+// hold SRT_GW5_BLOCK lanes (a multiple of 64 dividing 1280, the 20 waves 5 per SIMD make): with 640, two
+// blocks per CU, so the tree's top levels are copied into LDS twice per CU instead of five times and the
+// LDS a block may take beside its rings (80 KB) holds one level more
+#ifndef SRT_GW5_BLOCK
+#define SRT_GW5_BLOCK 256
+#endif
+constexpr int kGw5Block = SRT_GW5_BLOCK;
+static_assert(kGw5Block % 64 == 0 && 1280 % kGw5Block == 0, "SRT_GW5_BLOCK: 64-lane waves, 1280 lanes per CU");
+// Lanes per block of a global-scene launch of `gw` waves per SIMD (timed fused instance or not)
+constexpr int GlobalBlock(bool timed_fused, int gw) { return (timed_fused && gw == 5) ? kGw5Block : 256; }
+// The LDS one such block may take: its share of the CU's 160 KiB at gw waves per SIMD (4 SIMDs x 64 lanes)
+constexpr size_t GlobalBlockLds(int block, int gw) { return kLdsBytes * (size_t)block / ((size_t)gw * 256); }
 
 template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX, bool FUSE = false, int GW = 4>
 int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
@@ -511,6 +527,8 @@ int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
     c->occupancy.push_back({fn, lds, per_cu});
   }
   const int blocks = c->num_cus * per_cu;
+  c->launch_per_cu = per_cu;
+  c->launch_block = BLOCK;
   if constexpr (!LDSM) {  // global-scene mode: every lane's full stack in HBM (backing the LDS ring)
     const size_t lanes = (size_t)blocks * BLOCK;
     const size_t need = lanes * (PACK ? 2 : 3) * sizeof(uint32_t) * (size_t)kp.stack_entries;
@@ -602,8 +620,8 @@ int LaunchMode(srt_context* c, const srt::KParams& kc, size_t lds, bool count, b
   if (count) return pack ? LaunchSamples<true, false, true, 256, TEX>(c, kc, lds)
                          : LaunchSamples<true, false, false, 256, TEX>(c, kc, lds);
   if (ldsm) return LaunchSamples<false, true, true, kLdsBlock, TEX>(c, kc, lds);
-  if (c->fused && c->global_waves == 5) return pack ? LaunchSamples<false, false, true, 256, TEX, true, 5>(c, kc, lds)
-                                                   : LaunchSamples<false, false, false, 256, TEX, true, 5>(c, kc, lds);
+  if (c->fused && c->global_waves == 5) return pack ? LaunchSamples<false, false, true, kGw5Block, TEX, true, 5>(c, kc, lds)
+                                                   : LaunchSamples<false, false, false, kGw5Block, TEX, true, 5>(c, kc, lds);
   if (c->fused) return pack ? LaunchSamples<false, false, true, 256, TEX, true>(c, kc, lds)
                             : LaunchSamples<false, false, false, 256, TEX, true>(c, kc, lds);
   return pack ? LaunchSamples<false, false, true, 256, TEX>(c, kc, lds)
@@ -838,6 +856,14 @@ int LaunchWavefront(srt_context* c, srt::KParams kp, bool tex) {
   return SRT_OK;
 }
 
+// LDS bytes of the light and material records a launch keeps in LDS (behind the rest of its layout; each
+// when it fits the kernel's cap, as Launch places them)
+size_t LightMatLdsBytes(const srt_context* c, const srt::KParams& kp) {
+  const size_t light_bytes = 2 * sizeof(float4) * ((size_t)kp.light_records + 1);
+  const size_t mat_bytes = 2 * sizeof(float4) * ((size_t)c->n_mats + 1);
+  return (light_bytes <= 8192 ? light_bytes : 0) + (kp.show_model && c->d_mats && mat_bytes <= 16384 ? mat_bytes : 0);
+}
+
 // Runs frames kp.frame_first .. + kp.nframes - 1 (or the reset frame) through
 // sample_kernel + accumulate_kernel, in chunks that fit the sample buffer.
 int Launch(srt_context* c, srt::KParams& kp, bool count) {
@@ -855,7 +881,8 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   const size_t scene_bytes = ((size_t)kp.nodes_lds_f4 + (size_t)kp.tris_f4) * sizeof(float4);
   const size_t lds_mode_bytes = scene_bytes + (size_t)kLdsBlock * 2 * sizeof(uint32_t) * (size_t)kp.stack_entries;
   const bool ldsm = kp.show_model && c->lds_ok && c->pairs_aligned && !c->force_global && lds_mode_bytes <= kLdsBytes;
-  const int block = ldsm ? kLdsBlock : 256;
+  const int gw = (!count && c->fused) ? c->global_waves : 4;  // global-scene mode: LaunchMode's instance
+  const int block = ldsm ? kLdsBlock : GlobalBlock(!count && c->fused, gw);
   // pool mode (pool.hpp): LDS mode with stacks for the traversal waves only, then the ray records;
   // laid out first, and sample_kernel's layout when the records do not fit
   bool pool = ldsm && c->pool && !c->sample_textures && kp.max_depth >= 0 && kp.max_depth <= 255;
@@ -869,7 +896,6 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
       lds = lds_mode_bytes;
     } else if (kp.show_model) {  // LDS rings of global_ring(waves) entries per lane, backed by HBM stacks
       kp.stack_base_f4 = 0;
-      const int gw = (!count && c->fused) ? c->global_waves : 4;  // LaunchMode's instance
       lds = (size_t)block * (c->lds_ok ? 2 : 3) * sizeof(uint32_t) * (size_t)srt::global_ring(gw);
       if (SRT_COOP && !count && c->fused) {  // the fused sub-steps' load stages, one per wave
         lds = (lds + 15) & ~(size_t)15;
@@ -877,14 +903,15 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
         lds += (size_t)(block / 64) * srt::kCoopWaveBytes;
       }
       // the top levels' pairs (LayoutNodes' first region) for the fused instance, when they fit beside the
-      // rings within the LDS one of the instance's gw blocks per CU may take (2 KB left for lights and
-      // materials); wavefront mode's kernels read none
+      // rings and this launch's light and material records (placed behind it, below) within the LDS one
+      // of the instance's gw blocks per CU may take, so the region never costs a block per CU;
+      // wavefront mode's kernels read none
       kp.top_f4 = 0;
       const bool wf_launch = !count && (c->wavefront >= 0 ? c->wavefront == 1 : c->wf_scene);
       if (!count && c->fused && !wf_launch && c->top_f4 > 0) {
         lds = (lds + 15) & ~(size_t)15;
         const size_t tb = ((size_t)c->top_f4 + 3) / 4 * srt::kNodeBlkF4 * sizeof(float4);
-        if (lds + tb + 2048 <= kLdsBytes / (size_t)gw) {
+        if (lds + tb + LightMatLdsBytes(c, kp) <= GlobalBlockLds(block, gw)) {
           kp.top_f4 = c->top_f4;
           kp.top_lds_f4 = (int)(lds / sizeof(float4));
           lds += tb;
@@ -982,6 +1009,7 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
   // stream.  A piped chunk's batch counter is the slot's one word (its previous launch is accumulated).
   const int ctr_need = piped ? 1 : nchunks;
   const bool overlap = c->pipe_overlap == 2 || (c->pipe_overlap == 1 && c->nranks > 1);
+  c->launch_overlap = piped && overlap;
   if (piped || (count && c->pipe > 1)) {  // every slot's sample buffer now: a timed loop allocates none
     for (auto& sl : c->slots) {
       if (sl.lbuf_bytes >= need) continue;
@@ -1253,6 +1281,52 @@ bool LayoutNodes(const srt_bvh_node* nodes, uint32_t n_nodes, const srt_bvh_reco
   }
   if (top_depth <= 0 && n_top_slots) *n_top_slots = 0;
   *n_slots = next;
+  return true;
+}
+
+// The slots LayoutNodes(..., top_depth) gives its top region: its first pass alone (the pairs of the nodes
+// at depth < top_depth, bounded by the depth, not the tree's size); false where LayoutNodes would fail.
+bool TopRegionSlots(const srt_bvh_node* nodes, uint32_t n_nodes, const srt_bvh_record* bvhs, uint32_t n_bvhs,
+                    bool align, int top_depth, uint32_t* n_top) {
+  std::unordered_map<uint32_t, uint32_t> m;  // the few nodes the pass places -> slot
+  m[0] = 0;
+  uint32_t next = 1;
+  std::vector<uint32_t> roots{0};
+  for (uint32_t b = 0; b < n_bvhs; ++b) {
+    const uint32_t r = bvhs[b].first_index;
+    if (!m.count(r)) {
+      m[r] = next;
+      next += 2;
+    }
+    roots.push_back(r);
+  }
+  constexpr uint32_t kUnset = 0xFFFFFFFFu;
+  uint32_t chain_next = kUnset;
+  std::vector<std::pair<uint32_t, int>> st;
+  for (uint32_t r : roots) {
+    st.push_back({r, 0});
+    while (!st.empty()) {
+      const uint32_t i = st.back().first;
+      const int d = st.back().second;
+      st.pop_back();
+      const srt_bvh_node& n = nodes[i];
+      if (n.prim_count > 0 || d >= top_depth) continue;
+      const uint32_t c0 = n.first_child_or_prim_index, c1 = c0 + 1;
+      const auto f0 = m.find(c0), f1 = m.find(c1);
+      if (f0 == m.end() && f1 == m.end()) {
+        if (align && i != chain_next && nodes[c1].prim_count == 0 && (next & 3u) != 3u) next += 2;
+        m[c0] = next;
+        m[c1] = next + 1;
+        next += 2;
+        chain_next = nodes[c1].prim_count == 0 ? c1 : kUnset;
+        st.push_back({c0, d + 1});
+        st.push_back({c1, d + 1});
+      } else if (f0 == m.end() || f1 == m.end() || f1->second != f0->second + 1) {
+        return false;
+      }
+    }
+  }
+  *n_top = next;
   return true;
 }
 
@@ -1533,7 +1607,9 @@ int srt_get_int(srt_context* c, const char* name, int* v) {
   else if (n == "scene.treelets") *v = (int)c->n_treelets;
   else if (n == "scene.tri_slots") *v = (int)c->n_tris;  // device triangle records (LayoutTris gaps included)
   else if (n == "launch.chunks") *v = c->ev_used / 2;   // sample launches of the last render or dispatch
-  else if (n == "launch.overlap") *v = (c->pipe > 1 && (c->pipe_overlap == 2 || (c->pipe_overlap == 1 && c->nranks > 1))) ? 1 : 0;
+  else if (n == "launch.overlap") *v = c->launch_overlap ? 1 : 0;  // what the last render's launches did
+  else if (n == "launch.blocks_per_cu") *v = c->launch_per_cu;      // resident blocks per CU of the last sample launch
+  else if (n == "launch.block") *v = c->launch_block;               // its lanes per block
   else return SRT_ERR_NOT_FOUND;
   return SRT_OK;
 }
@@ -1780,31 +1856,6 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   // Crossover taken at 48 MB; SRT_GLOBAL_WAVES_MODE=4/5 forces either.
   const char* gw_env = std::getenv("SRT_GLOBAL_WAVES_MODE");
   c->global_waves = gw_env ? (gw_env[0] == '5' ? 5 : 4) : (scene_mb < 48.0 ? 5 : 4);
-  // The fused instance's LDS copy of the tree's top levels (traversal.hpp trav_fused): LDS reads bypass
-  // the vector-memory pipeline that bounds these kernels (DESIGN.md section 5).  Laid out first, as deep
-  // as fits the LDS one block may take beside its rings (SRT_TOP_DEPTH=d forces d levels, 0 none).
-  uint32_t n_top = 0;
-  int top_depth = 0;
-  {
-    const char* td_env = std::getenv("SRT_TOP_DEPTH");
-    if (c->fused && scene_mb >= 1.0 && !(td_env && std::atoi(td_env) <= 0)) {
-      const bool pack = 3ull * n_tris < (1ull << 24) && (uint64_t)n_nodes + srt::kNodePad < (1ull << 24);
-      const size_t ring = (size_t)256 * (pack ? 2 : 3) * sizeof(uint32_t) * (size_t)srt::global_ring(c->global_waves);
-      const size_t budget = kLdsBytes / (size_t)c->global_waves - ring - 2048;
-      top_depth = td_env ? std::atoi(td_env) : 12;
-      for (; top_depth > 0; --top_depth) {  // the deepest whole levels that fit
-        uint32_t ns = 0;
-        if (!LayoutNodes(nodes, n_nodes, bvhs, n_bvhs, align, &remap, &ns, top_depth, &n_top)) {
-          top_depth = 0;
-          break;
-        }
-        if (td_env || ((2 * (size_t)n_top + 2 + 3) / 4) * srt::kNodeBlkF4 * sizeof(float4) <= budget) break;
-      }
-    }
-  }
-  bool laid = !(lay_env && lay_env[0] == '0') &&
-              LayoutNodes(nodes, n_nodes, bvhs, n_bvhs, align, &remap, &n_slots, top_depth, &n_top);
-  if (!laid) n_top = 0;
   // Triangle slots (LayoutTris) for every scene read through L2 (none of 1 MB fits the LDS copy):
   // fewer lines per leaf step (A/B on one box, kernel ms: C5 10 M 4096² 820 -> 773 with the IL leaf
   // step's own-record reads, 3 M 58.4 -> 56.5, 1 M 34.1 -> 32.6, torus knot 27.4 -> 27.4, Rubik
@@ -1817,6 +1868,42 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   // (the slots stay below 3 n_tris: a gap is at most two records per leaf)
   const bool tris_laid =
       tri_align && n_tris < (1u << 30) && LayoutTris(nodes, n_nodes, reach, n_tris, &tslot, &n_tslots);
+  uint32_t max_leaf = 0;
+  for (uint32_t i = 0; i < n_nodes; ++i)
+    if (reach[i]) max_leaf = std::max(max_leaf, nodes[i].prim_count);
+  // The fused instance's LDS copy of the tree's top levels (traversal.hpp trav_fused): LDS reads bypass
+  // the vector-memory pipeline that bounds these kernels (DESIGN.md section 5).  Laid out first, as deep
+  // as fits the LDS one block may take beside its rings and the light and material records
+  // (SRT_TOP_DEPTH=d forces d levels, 0 none).  The ring's entry size is the one Launch will use
+  // (lds_ok below, with the dense node count: a line-aligned layout's padding only matters past 2^24
+  // slots, where Launch then finds the region too large and skips it).  A depth's region size comes from
+  // the layout's first pass alone (TopRegionSlots, bounded by the depth); the full layout runs once.
+  uint32_t n_top = 0;
+  int top_depth = 0;
+  {
+    const char* td_env = std::getenv("SRT_TOP_DEPTH");
+    if (c->fused && scene_mb >= 1.0 && !(td_env && std::atoi(td_env) <= 0)) {
+      const bool pack = n_tslots < (1u << 24) && n_nodes + srt::kNodePad < (1u << 24) && max_leaf < 256;
+      const int gblock = GlobalBlock(true, c->global_waves);
+      const size_t ring = (size_t)gblock * (pack ? 2 : 3) * sizeof(uint32_t) * (size_t)srt::global_ring(c->global_waves);
+      // lights: the ones set, at least the reference's six (src/main.cpp:584-589), + the zero record
+      const size_t lm = 2 * sizeof(float4) * (std::max<size_t>(c->h_lights.size(), 6) + 1) +
+                        2 * sizeof(float4) * ((size_t)n_mats + 1);
+      const size_t share = GlobalBlockLds(gblock, c->global_waves);
+      const size_t budget = share > ring + lm + 64 ? share - ring - lm - 64 : 0;
+      top_depth = td_env ? std::atoi(td_env) : 12;
+      for (; top_depth > 0; --top_depth) {  // the deepest whole levels that fit
+        if (!TopRegionSlots(nodes, n_nodes, bvhs, n_bvhs, align, top_depth, &n_top)) {
+          top_depth = 0;
+          break;
+        }
+        if (td_env || ((2 * (size_t)n_top + 2 + 3) / 4) * srt::kNodeBlkF4 * sizeof(float4) <= budget) break;
+      }
+    }
+  }
+  bool laid = !(lay_env && lay_env[0] == '0') &&
+              LayoutNodes(nodes, n_nodes, bvhs, n_bvhs, align, &remap, &n_slots, top_depth, &n_top);
+  if (!laid) n_top = 0;
   auto tsl = [&](uint32_t t) { return tris_laid ? tslot[t] : t; };
   for (auto& r : tri_ranges)
     if (r.first < r.second) r = {tsl(r.first), tsl(r.second - 1) + 1};
@@ -2001,9 +2088,6 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
   c->n_tris = n_tslots;  // device records (slots)
   c->n_mats = n_mats;
   c->stack_entries = depth + 1;
-  uint32_t max_leaf = 0;
-  for (uint32_t i = 0; i < n_nodes; ++i)
-    if (reach[i]) max_leaf = std::max(max_leaf, nodes[i].prim_count);
   c->lds_ok = n_tslots < (1u << 24) && n_slots + srt::kNodePad < (1u << 24) && max_leaf < 256;
   // cooperative loads (SRT_COOP builds) carry a request's float4 index in kCoopIdxBits bits: larger
   // arrays (only reachable with SRT_GLOBAL_FUSED_MODE=1 past 600 MB) take the IL instance

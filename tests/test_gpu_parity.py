@@ -312,6 +312,39 @@ def test_top_levels_in_lds(monkeypatch, depth):
     assert_parity(two, 2)
 
 
+@pytest.mark.parametrize("n_mats,min_depth", [(1, 7), (100, 7), (400, 4), (600, 7)])
+def test_top_region_keeps_occupancy_with_many_materials(n_mats, min_depth):
+    """the top levels' LDS region is sized beside the rings AND the launch's actual light and
+    material records (placed behind it in the same block's LDS), so many materials never cost the 5-wave
+    fused instance a block per CU: the knot (5 waves per SIMD, 256-lane blocks) keeps 5 resident blocks per
+    CU with 1, 100, 400 (12.8 KB of records in LDS: the region shrinks to make room) and 600 materials
+    (past the 16-KB LDS cap: the records stay in HBM and the region keeps its depth); the frame matches
+    the oracle."""
+    import dataclasses
+
+    base = R.make_setup(48, 40, show_model=True, models=[R.torus_knot_model()])
+    sc = base.scene
+    mats = np.resize(sc.mats, n_mats).copy()
+    mats["diffuse"] = np.stack([np.linspace(0.2, 0.9, n_mats), np.linspace(0.9, 0.3, n_mats),
+                                np.full(n_mats, 0.5)], axis=1).astype(np.float32)
+    tris = sc.tris.copy()
+    tris["mat"] = np.arange(len(tris), dtype=np.uint32) % n_mats
+    scene = dataclasses.replace(sc, mats=mats, tex_albedo=np.resize(sc.tex_albedo, (n_mats, 3)).copy(), tris=tris)
+    setup = dataclasses.replace(base, scene=scene)
+    r = R.Renderer(setup)
+    try:
+        c = r.compute
+        assert c.GetInt("scene.fused") == 1 and c.GetInt("scene.global_waves") == 5
+        r.render(1)
+        r.finish()
+        assert c.GetInt("launch.block") == 256 and c.GetInt("launch.blocks_per_cu") == 5
+        assert c.GetInt("launch.top_f4") == c.GetInt("scene.top_f4") > 0
+        assert c.GetInt("scene.top_depth") >= min_depth
+    finally:
+        r.close()
+    assert_parity(setup, 2)
+
+
 @pytest.mark.parametrize("case", ["overlap", "shared"])
 def test_triangle_slots_unusual_leaves(case):
     """LayoutTris on leaf ranges no reference-built tree has: a leaf grown by one triangle into the next
