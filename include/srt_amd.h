@@ -171,7 +171,9 @@ int srt_local_rows(srt_context* ctx);
  *   "launch.top_f4"      the top region its global-scene launch copied (0: none: the region did not fit
  *                        beside the rings and the light and material records);
  *   "launch.blocks_per_cu", "launch.block"  resident blocks per CU and lanes per block of its last
- *                        sample launch. */
+ *                        sample launch;
+ *   "launch.mats_lds"    1 when that launch read the material records from LDS (0: from HBM, where they
+ *                        did not fit the LDS its blocks may take). */
 int srt_device(srt_context* ctx);
 int srt_get_int(srt_context* ctx, const char* name, int* v);
 

@@ -106,6 +106,7 @@ struct srt_context {
   int launch_top_f4 = 0;           // the region the last global-scene launch copied (0: none)
   bool launch_overlap = false;     // the last render's sample launches ran piped and overlapped (launch.overlap)
   int launch_per_cu = 0, launch_block = 0;  // resident blocks per CU and lanes per block of the last sample launch
+  int launch_mats_lds = 0;                  // the last launch read the material records from LDS
   int global_waves = 4;       // the fused instance's waves per SIMD (set at upload: 5 for small trees)
   // lights
   std::vector<srt_light> h_lights;
@@ -856,12 +857,11 @@ int LaunchWavefront(srt_context* c, srt::KParams kp, bool tex) {
   return SRT_OK;
 }
 
-// LDS bytes of the light and material records a launch keeps in LDS (behind the rest of its layout; each
-// when it fits the kernel's cap, as Launch places them)
-size_t LightMatLdsBytes(const srt_context* c, const srt::KParams& kp) {
+// LDS bytes of the light records a launch keeps in LDS (behind the rest of its layout, when they fit the
+// kernel's cap, as Launch places them)
+size_t LightLdsBytes(const srt::KParams& kp) {
   const size_t light_bytes = 2 * sizeof(float4) * ((size_t)kp.light_records + 1);
-  const size_t mat_bytes = 2 * sizeof(float4) * ((size_t)c->n_mats + 1);
-  return (light_bytes <= 8192 ? light_bytes : 0) + (kp.show_model && c->d_mats && mat_bytes <= 16384 ? mat_bytes : 0);
+  return light_bytes <= 8192 ? light_bytes : 0;
 }
 
 // Runs frames kp.frame_first .. + kp.nframes - 1 (or the reset frame) through
@@ -903,15 +903,16 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
         lds += (size_t)(block / 64) * srt::kCoopWaveBytes;
       }
       // the top levels' pairs (LayoutNodes' first region) for the fused instance, when they fit beside the
-      // rings and this launch's light and material records (placed behind it, below) within the LDS one
-      // of the instance's gw blocks per CU may take, so the region never costs a block per CU;
-      // wavefront mode's kernels read none
+      // rings and this launch's light records (placed behind it, below) within the LDS one of the
+      // instance's blocks may take; the material records follow only if they still fit that share, else
+      // shading reads them from HBM, so neither costs a resident block per CU, and the region,
+      // worth ~10% on a surface mesh, is never given up for them; wavefront mode's kernels read none
       kp.top_f4 = 0;
       const bool wf_launch = !count && (c->wavefront >= 0 ? c->wavefront == 1 : c->wf_scene);
       if (!count && c->fused && !wf_launch && c->top_f4 > 0) {
         lds = (lds + 15) & ~(size_t)15;
         const size_t tb = ((size_t)c->top_f4 + 3) / 4 * srt::kNodeBlkF4 * sizeof(float4);
-        if (lds + tb + LightMatLdsBytes(c, kp) <= GlobalBlockLds(block, gw)) {
+        if (lds + tb + LightLdsBytes(kp) <= GlobalBlockLds(block, gw)) {
           kp.top_f4 = c->top_f4;
           kp.top_lds_f4 = (int)(lds / sizeof(float4));
           lds += tb;
@@ -922,21 +923,25 @@ int Launch(srt_context* c, srt::KParams& kp, bool count) {
       kp.stack_base_f4 = 0;
       lds = 0;
     }
-    {  // light and material records in LDS behind the rest, when they fit (shading reads them there)
+    {  // light and material records in LDS behind the rest, when they fit (shading reads them there) within
+       // the LDS one block may take: all of it in LDS mode, a global-scene block's share at its instance's
+       // blocks per CU (records past it would cost a resident block per CU; they are read from HBM instead)
+      const size_t cap = (!ldsm && kp.show_model) ? GlobalBlockLds(block, gw) : kLdsBytes;
       lds = (lds + 15) & ~(size_t)15;
       const size_t light_bytes = 2 * sizeof(float4) * ((size_t)kp.light_records + 1);
-      kp.lights_lds = (light_bytes <= 8192 && lds + light_bytes <= kLdsBytes) ? 1 : 0;
+      kp.lights_lds = (light_bytes <= 8192 && lds + light_bytes <= cap) ? 1 : 0;
       if (kp.lights_lds) {
         kp.lights_base_f4 = (int)(lds / sizeof(float4));
         lds += light_bytes;
       }
       kp.mat_records = (int)c->n_mats + 1;
       const size_t mat_bytes = 2 * sizeof(float4) * (size_t)kp.mat_records;
-      kp.mats_lds = (kp.show_model && c->d_mats && mat_bytes <= 16384 && lds + mat_bytes <= kLdsBytes) ? 1 : 0;
+      kp.mats_lds = (kp.show_model && c->d_mats && mat_bytes <= 16384 && lds + mat_bytes <= cap) ? 1 : 0;
       if (kp.mats_lds) {
         kp.mats_base_f4 = (int)(lds / sizeof(float4));
         lds += mat_bytes;
       }
+      c->launch_mats_lds = kp.mats_lds;
     }
     if (!pool) break;
     // control words, 3 rings of u32 record ids (power-of-two capacity), 112-B records
@@ -1610,6 +1615,7 @@ int srt_get_int(srt_context* c, const char* name, int* v) {
   else if (n == "launch.overlap") *v = c->launch_overlap ? 1 : 0;  // what the last render's launches did
   else if (n == "launch.blocks_per_cu") *v = c->launch_per_cu;      // resident blocks per CU of the last sample launch
   else if (n == "launch.block") *v = c->launch_block;               // its lanes per block
+  else if (n == "launch.mats_lds") *v = c->launch_mats_lds;          // 1: it read the material records from LDS
   else return SRT_ERR_NOT_FOUND;
   return SRT_OK;
 }
@@ -1873,8 +1879,8 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
     if (reach[i]) max_leaf = std::max(max_leaf, nodes[i].prim_count);
   // The fused instance's LDS copy of the tree's top levels (traversal.hpp trav_fused): LDS reads bypass
   // the vector-memory pipeline that bounds these kernels.  Laid out first, as deep
-  // as fits the LDS one block may take beside its rings and the light and material records
-  // (SRT_TOP_DEPTH=d forces d levels, 0 none).  The ring's entry size is the one Launch will use
+  // as fits the LDS one block may take beside its rings and the light records (SRT_TOP_DEPTH=d forces d
+  // levels, 0 none).  The ring's entry size is the one Launch will use
   // (lds_ok below, with the dense node count: a line-aligned layout's padding only matters past 2^24
   // slots, where Launch then finds the region too large and skips it).  A depth's region size comes from
   // the layout's first pass alone (TopRegionSlots, bounded by the depth); the full layout runs once.
@@ -1886,9 +1892,11 @@ int srt_upload_scene(srt_context* c, const srt_bvh_record* bvhs, uint32_t n_bvhs
       const bool pack = n_tslots < (1u << 24) && n_nodes + srt::kNodePad < (1u << 24) && max_leaf < 256;
       const int gblock = GlobalBlock(true, c->global_waves);
       const size_t ring = (size_t)gblock * (pack ? 2 : 3) * sizeof(uint32_t) * (size_t)srt::global_ring(c->global_waves);
-      // lights: the ones set, at least the reference's six (src/main.cpp:584-589), + the zero record
-      const size_t lm = 2 * sizeof(float4) * (std::max<size_t>(c->h_lights.size(), 6) + 1) +
-                        2 * sizeof(float4) * ((size_t)n_mats + 1);
+      // beside the light records (the ones set, at least the reference's six, src/main.cpp:584-589, and the
+      // zero record) when they fit their LDS cap, as Launch places them (LightLdsBytes); the material
+      // records take what the region leaves (Launch)
+      const size_t lb = 2 * sizeof(float4) * (std::max<size_t>(c->h_lights.size(), 6) + 1);
+      const size_t lm = lb <= 8192 ? lb : 0;
       const size_t share = GlobalBlockLds(gblock, c->global_waves);
       const size_t budget = share > ring + lm + 64 ? share - ring - lm - 64 : 0;
       top_depth = td_env ? std::atoi(td_env) : 12;

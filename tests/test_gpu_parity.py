@@ -312,16 +312,15 @@ def test_top_levels_in_lds(monkeypatch, depth):
     assert_parity(two, 2)
 
 
-@pytest.mark.parametrize("n_mats,min_depth", [(1, 7), (100, 7), (400, 4), (600, 7)])
-def test_top_region_keeps_occupancy_with_many_materials(n_mats, min_depth):
-    """the top levels' LDS region is sized beside the rings AND the launch's actual light and
-    material records (placed behind it in the same block's LDS), so many materials never cost the 5-wave
-    fused instance a block per CU: the knot (5 waves per SIMD, 256-lane blocks) keeps 5 resident blocks per
-    CU with 1, 100, 400 (12.8 KB of records in LDS: the region shrinks to make room) and 600 materials
-    (past the 16-KB LDS cap: the records stay in HBM and the region keeps its depth); the frame matches
-    the oracle."""
-    import dataclasses
-
+@pytest.mark.parametrize("n_mats,mats_in_lds", [(1, True), (100, True), (150, True), (200, False), (600, False)])
+def test_top_region_keeps_occupancy_with_many_materials(n_mats, mats_in_lds):
+    """the top levels' LDS region is sized beside the rings and the launch's light records, and
+    the material records (placed behind it in the same block's LDS) only go there when they still fit the
+    block's share, so many materials never cost the 5-wave fused instance a resident block per CU, and never
+    its region either: the knot (5 waves per SIMD, 256-lane blocks) keeps 5 blocks per CU and its 7-level
+    region with 1 to 600 materials; up to 150 (4.8 KB of records) sit in LDS beside the 16-KB rings, the
+    10-KB region and the lights, 200 and 600 are read from HBM (6.4 KB: past the 32-KB share; 19.2 KB: also
+    past the 16-KB LDS cap); the frame matches the oracle."""
     base = R.make_setup(48, 40, show_model=True, models=[R.torus_knot_model()])
     sc = base.scene
     mats = np.resize(sc.mats, n_mats).copy()
@@ -338,8 +337,8 @@ def test_top_region_keeps_occupancy_with_many_materials(n_mats, min_depth):
         r.render(1)
         r.finish()
         assert c.GetInt("launch.block") == 256 and c.GetInt("launch.blocks_per_cu") == 5
-        assert c.GetInt("launch.top_f4") == c.GetInt("scene.top_f4") > 0
-        assert c.GetInt("scene.top_depth") >= min_depth
+        assert c.GetInt("launch.top_f4") == c.GetInt("scene.top_f4") > 0 and c.GetInt("scene.top_depth") >= 7
+        assert c.GetInt("launch.mats_lds") == int(mats_in_lds)
     finally:
         r.close()
     assert_parity(setup, 2)
