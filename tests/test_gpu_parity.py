@@ -321,6 +321,8 @@ def test_top_region_keeps_occupancy_with_many_materials(n_mats, mats_in_lds):
     region with 1 to 600 materials; up to 150 (4.8 KB of records) sit in LDS beside the 16-KB rings, the
     10-KB region and the lights, 200 and 600 are read from HBM (6.4 KB: past the 32-KB share; 19.2 KB: also
     past the 16-KB LDS cap); the frame matches the oracle."""
+    import dataclasses
+
     base = R.make_setup(48, 40, show_model=True, models=[R.torus_knot_model()])
     sc = base.scene
     mats = np.resize(sc.mats, n_mats).copy()
