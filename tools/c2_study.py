@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""Reduces a counter study's runs into JSON: tools/c2_study.sh (gpurun_out/c2s/b<N>/, one per
+"""Reduces a counter study's runs into JSON: tools/probes/c2_study.sh (gpurun_out/c2s/b<N>/, one per
 sphere_kernel occupancy) or tools/pmc_study.sh (gpurun_out/<name>/<variant>/, --kernel PREFIX): for each,
 the timed launch's kernel time and its counters, per launch.
 

@@ -5,14 +5,14 @@ hit samples its texture: the TEX instance) and without (the reference's loader: 
 albedo per material).  Prints the sample-kernel time per render (srt_kernel_time, 3 renders back to back)
 and the counted rays of each.
 
-  python tools/airplane_probe.py [spp]
+  python tools/probes/airplane_probe.py [spp]
 """
 import pathlib
 import shutil
 import sys
 import tempfile
 
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd"))
 sys.path.insert(0, str(ROOT))
 

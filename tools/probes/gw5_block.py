@@ -1,6 +1,6 @@
 """Probe: resident blocks per CU of the 5-wave fused instance at its build's block size (SRT_GW5_BLOCK)."""
 import sys, pathlib
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd")); sys.path.insert(0, str(ROOT))
 from srt_amd import render as R
 r = R.Renderer(R.make_setup(480, 270, show_model=True, models=[R.torus_knot_model()]))

@@ -1,7 +1,7 @@
 """Diagnostic: phase split of sample_kernel (needs the SRT_PHASE_TIMING build via SRT_LIB_PATH; the
 per-sub-step lines need -DSRT_SUBSTEP_STATS too, whose atomics distort the timing)."""
 import ctypes as C, sys, pathlib, os
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd")); sys.path.insert(0, str(ROOT))
 import srt_amd as S
 from srt_amd import render as R, _lib

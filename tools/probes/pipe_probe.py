@@ -2,14 +2,14 @@
 pipelined sample launches (SRT_PIPELINE): host wall time per render over `steps` renders enqueued
 without a synchronisation between them, as bench.py's timed loop enqueues its steps.
 
-Usage: python tools/pipe_probe.py [nranks] [spp] [steps] [scene]   (run once per SRT_PIPELINE value)
+Usage: python tools/probes/pipe_probe.py [nranks] [spp] [steps] [scene]   (run once per SRT_PIPELINE value)
 """
 import os
 import pathlib
 import sys
 import time
 
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd"))
 sys.path.insert(0, str(ROOT))
 

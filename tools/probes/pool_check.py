@@ -1,6 +1,6 @@
 """Development probe for pool_kernel (pool.hpp): oracle parity on small Rubik frames (counting and
 timed instances, per-frame dispatches), then the metric frame with and without pools, bitwise and timed.
-usage: python tools/pool_check.py [spp_big]   (runs with SRT_POOL toggled per context)"""
+usage: python tools/probes/pool_check.py [spp_big]   (runs with SRT_POOL toggled per context)"""
 import os
 import pathlib
 import sys
@@ -8,7 +8,7 @@ import time
 
 import numpy as np
 
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 for p in (ROOT / "simple-ray-tracer_amd", ROOT, ROOT / "tests"):
     sys.path.insert(0, str(p))
 from srt_amd import render as R  # noqa: E402

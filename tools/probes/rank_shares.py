@@ -4,12 +4,12 @@ library's HIP events.  A node of N GPUs finishes the sample kernel when its slow
 max over ranks of the share's kernel time predicts the N-GPU step (before the gather, which moves
 W*H*16 B / N per rank).
 
-Usage: python tools/rank_shares.py [spp] [band_rows] [scene]
+Usage: python tools/probes/rank_shares.py [spp] [band_rows] [scene]
 """
 import pathlib
 import sys
 
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd"))
 sys.path.insert(0, str(ROOT))
 

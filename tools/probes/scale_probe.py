@@ -4,13 +4,13 @@ rank's share of an N-GPU split (2-row bands), at the build's defaults (launches 
 multi-rank share, section 5 of DESIGN.md).  A share's time bounds its rank's step; the gather of the
 sRGB8 rows (4 B/px) and the assembly on rank 0 come on top on a real node.
 
-Usage: python tools/scale_probe.py [steps] [band_rows]  (all ranks' shares at N = 8 with a third argument "all")
+Usage: python tools/probes/scale_probe.py [steps] [band_rows]  (all ranks' shares at N = 8 with a third argument "all")
 """
 import pathlib
 import sys
 import time
 
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd"))
 sys.path.insert(0, str(ROOT))
 

@@ -12,7 +12,7 @@
  * Input (binary, little endian): u32 n_nodes, u32 n_tris, u32 n_rays; n_nodes x 32-B std430 BVHNode
  * (min xyz, first, max xyz, count); n_tris x 9 f32 (v0 v1 v2, BVH order); n_rays x 7 f32 (o, d, tmax).
  * Output: one line per order: rays, occluded, mean node pairs, mean triangle tests.
- *   gcc -O2 -o /tmp/shadow_order tools/shadow_order.c -lm && /tmp/shadow_order rays.bin   (tools/shadow_order.py)
+ *   gcc -O2 -o /tmp/shadow_order tools/probes/shadow_order.c -lm && /tmp/shadow_order rays.bin   (tools/probes/shadow_order.py)
  */
 #include <math.h>
 #include <stdint.h>

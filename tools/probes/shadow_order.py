@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
 """Diagnostic: how many traversal steps a shadow ray takes under the reference's child order, nearer-first
-and farther-first (tools/shadow_order.c), and how many fused sub-steps (memory round trips) under the
-kernel's schedule and under schedules that expand the stack's top entry in the same step (tools/shadow_steps.c).  Shadow rays (CheckLightOccluded) only need CheckHit(...).hit,
+and farther-first (tools/probes/shadow_order.c), and how many fused sub-steps (memory round trips) under the
+kernel's schedule and under schedules that expand the stack's top entry in the same step (tools/probes/shadow_steps.c).  Shadow rays (CheckLightOccluded) only need CheckHit(...).hit,
 which does not depend on the visit order, so an any-hit walk may take either child first.
 
 The rays: the camera ray through each pixel centre of a W x H frame of the scene (model camera), its first
 hit (the oracle's closest-hit query), and from that point one shadow ray to each of the scene's lights.
 
-  python tools/shadow_order.py [torusknot|rubik] [W] [H]
+  python tools/probes/shadow_order.py [torusknot|rubik] [W] [H]
 """
 from __future__ import annotations
 
@@ -18,7 +18,7 @@ import tempfile
 
 import numpy as np
 
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd"))
 sys.path.insert(0, str(ROOT))
 
@@ -66,7 +66,7 @@ def main():
     print(f"{scene_name} {W}x{H}: {int(m.sum())} camera-ray hits x {len(lp)} lights = {len(sh)} shadow rays")
     for tool in ("shadow_order", "shadow_steps"):  # visit orders; fused sub-steps (round trips) per schedule
         exe = pathlib.Path(tempfile.gettempdir()) / tool
-        subprocess.run(["gcc", "-O2", "-o", str(exe), str(ROOT / "tools" / f"{tool}.c"), "-lm"], check=True)
+        subprocess.run(["gcc", "-O2", "-o", str(exe), str(ROOT / "tools" / "probes" / f"{tool}.c"), "-lm"], check=True)
         print(subprocess.run([str(exe), path], check=True, capture_output=True, text=True).stdout, end="")
     pathlib.Path(path).unlink()
 

@@ -11,8 +11,8 @@
  *               entry if it is internal (its pair in the spine's registers), pushing what that adds;
  *   schedule 2: as 1, and a leaf step whose leaf has one triangle left also expands an internal stack top
  *               (3 + 4 float4 of loads, within the step's 8).
- * Input: the binary of tools/shadow_order.py.  Output: mean sub-steps, node pairs and triangle tests per ray.
- *   gcc -O2 -o /tmp/shadow_steps tools/shadow_steps.c -lm
+ * Input: the binary of tools/probes/shadow_order.py.  Output: mean sub-steps, node pairs and triangle tests per ray.
+ *   gcc -O2 -o /tmp/shadow_steps tools/probes/shadow_steps.c -lm
  */
 #include <math.h>
 #include <stdint.h>

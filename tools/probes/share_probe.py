@@ -2,12 +2,12 @@
 the 1-GPU launch of the same batch count (spp / N frames of the whole image), and every rank's share
 (max against mean: imbalance between ranks).  Library HIP-event kernel times, best of 3.
 
-Usage: python tools/share_probe.py [N] [band_rows]
+Usage: python tools/probes/share_probe.py [N] [band_rows]
 """
 import pathlib
 import sys
 
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd"))
 sys.path.insert(0, str(ROOT))
 

@@ -3,7 +3,7 @@
 // section 3).  The reference's RNG (raytrace_utils.glsl:28-30) takes sin of dot(seed, (12.9898,
 // 78.233)) with |x| up to ~1e4, i.e. up to ~1600 revolutions.  For |x| in decades 1e0..1e5 this prints
 // the max / mean absolute error against sin in double, and how many results are exactly 0.
-// Build + run (GPU box): hipcc -O2 --offload-arch=gfx950 tools/sin_probe.hip -o /tmp/sin_probe && /tmp/sin_probe
+// Build + run (GPU box): hipcc -O2 --offload-arch=gfx950 tools/probes/sin_probe.hip -o /tmp/sin_probe && /tmp/sin_probe
 // TEST INFRASTRUCTURE (a measurement probe).
 #include <hip/hip_runtime.h>
 

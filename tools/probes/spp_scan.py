@@ -1,7 +1,7 @@
 """Kernel time vs spp for the metric frame (and one rank's share): the intercept of the linear fit
 is the per-launch fixed cost (fill + tail), the slope the steady-state cost per frame."""
 import pathlib, sys
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd")); sys.path.insert(0, str(ROOT))
 import numpy as np
 from srt_amd import render as R

@@ -5,12 +5,12 @@ L2 would then serve one strip's rays.)  Renders the 8 row-band shares of a 1920x
 other on one GPU, as 2-row bands dealt round robin (every share spans the frame) and as 135-row bands (each
 share one contiguous strip), and prints the rays per kernel time of each split.
 
-  python tools/strip_probe.py [scene: torusknot|airplane_knot|synthetic] [spp] [band rows, comma-separated: 2,135]
+  python tools/probes/strip_probe.py [scene: torusknot|airplane_knot|synthetic] [spp] [band rows, comma-separated: 2,135]
 """
 import pathlib
 import sys
 
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd"))
 sys.path.insert(0, str(ROOT))
 

@@ -1,7 +1,7 @@
 """Launch-latency probe: kernel time of tiny renders (one 8x8 batch = one wave's work, 64x64, the
 1080p frame) at 1 spp; the single-batch time is the latency of that wave's slowest path."""
 import pathlib, sys
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd")); sys.path.insert(0, str(ROOT))
 from srt_amd import render as R
 model = R.rubik_model(ROOT / "tests" / "golden" / "objects")

@@ -5,13 +5,13 @@ with the library's HIP events (best of 2).  A share of an 8-GPU split has 1/8 of
 so a window sized for the whole frame covers a large part of its launch, where every claim is one
 atomic on the launch's single counter.
 
-Usage: python tools/tail_sweep.py [scene] [spp] [band_rows] [tails, comma-separated]
+Usage: python tools/probes/tail_sweep.py [scene] [spp] [band_rows] [tails, comma-separated]
 """
 import os
 import pathlib
 import sys
 
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd"))
 sys.path.insert(0, str(ROOT))
 

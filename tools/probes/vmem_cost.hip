@@ -1,0 +1,89 @@
+// vmem_cost.hip -- what a divergent dwordx4 gather costs the vector-memory pipeline (TA / TD / L1) on
+// gfx950, as a function of the instruction's active lanes and of the distinct 128-B lines they touch.
+// Measurement probe for DESIGN.md section 5 (the global-scene kernels wait on TA/TD); not product code.
+//
+// Every lane of a wave reads 64-B records (4 x dwordx4, as a traversal step reads a node pair) from an
+// L2-resident table (2 MiB, so L1 misses and L2 hits, as the surface legs' loads mostly are).  Per case:
+//   A  lanes active (lane < A; the rest masked off by the branch),
+//   D  distinct lines per instruction (lane l reads line h(l % D), record (l / D) & 1 of its two),
+// and the time per load instruction per CU (all CUs busy: 8 waves per SIMD).
+//
+// build: hipcc -O3 --offload-arch=gfx950 -o tools/probes/vmem_cost tools/probes/vmem_cost.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                       \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) {                                                         \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      std::exit(1);                                                                 \
+    }                                                                               \
+  } while (0)
+
+__device__ __forceinline__ uint32_t mix32(uint32_t z) {
+  z = (z ^ (z >> 16)) * 0x7feb352du;
+  z = (z ^ (z >> 15)) * 0x846ca68bu;
+  return z ^ (z >> 16);
+}
+
+__global__ __launch_bounds__(256) void gather_kernel(const uint4* __restrict__ t, uint32_t n_lines, int iters,
+                                                     int A, int D, uint32_t* out) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  uint32_t acc = 0;
+  if (lane < A) {
+    const uint32_t grp = (uint32_t)(lane % D), rec = (uint32_t)((lane / D) & 1);
+    for (int it = 0; it < iters; ++it) {
+      const uint32_t line = mix32(wave * 0x9E3779B9u + (uint32_t)it * 0x85EBCA6Bu + grp * 0xC2B2AE35u) % n_lines;
+      const uint4* p = t + (size_t)line * 8 + rec * 4;  // 128-B line = 8 uint4, two 64-B records
+      const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+      acc ^= a.x ^ b.y ^ c.z ^ d.w ^ (a.w + b.x + c.y + d.z);
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;  // keeps the loads live
+}
+
+int main(int argc, char** argv) {
+  const size_t bytes = 2u << 20;
+  const uint32_t n_lines = (uint32_t)(bytes / 128);
+  uint4* t;
+  uint32_t* out;
+  CK(hipMalloc(&t, bytes));
+  CK(hipMalloc(&out, 4));
+  CK(hipMemset(t, 1, bytes));
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const int blocks = cus * 8;  // 256-lane blocks: 8 waves per SIMD
+  const int iters = 2000;
+  const int cases[][2] = {{64, 64}, {48, 48}, {32, 32}, {16, 16}, {8, 8}, {64, 32}, {64, 16}, {64, 8}, {32, 16}, {32, 8}};
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL(gather_kernel, dim3(blocks), dim3(256), 0, 0, t, n_lines, 50, 64, 64, out);  // warm-up
+  CK(hipDeviceSynchronize());
+  std::printf("{\"probe\": \"vmem_cost\", \"table_bytes\": %zu, \"cus\": %d, \"waves_per_simd\": 8, \"rows\": [\n", bytes, cus);
+  const int n = (int)(sizeof(cases) / sizeof(cases[0]));
+  for (int k = 0; k < n; ++k) {
+    const int A = cases[k][0], D = cases[k][1];
+    float best = 1e30f;
+    for (int rep = 0; rep < 3; ++rep) {
+      CK(hipEventRecord(e0));
+      hipLaunchKernelGGL(gather_kernel, dim3(blocks), dim3(256), 0, 0, t, n_lines, iters, A, D, out);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      best = ms < best ? ms : best;
+    }
+    const double instr_per_cu = (double)blocks * 4 * iters * 4 / cus;  // waves x iterations x 4 loads
+    const double ns = best * 1e6 / instr_per_cu;
+    std::printf("  {\"active_lanes\": %d, \"lines_per_instr\": %d, \"ms\": %.3f, \"ns_per_load_instr_per_cu\": %.4f, "
+                "\"cycles_at_2p4GHz\": %.2f}%s\n", A, D, best, ns, ns * 2.4, k + 1 < n ? "," : "");
+  }
+  std::printf("]}\n");
+  return 0;
+}

@@ -1,7 +1,7 @@
 """Per-wave timeline of one sample_kernel launch (diagnostic build with -DSRT_WAVE_TRACE, loaded via
 SRT_LIB_PATH): start, scene copied to LDS, batches exhausted, end -- s_memrealtime at 100 MHz."""
 import ctypes as C, pathlib, sys
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "simple-ray-tracer_amd")); sys.path.insert(0, str(ROOT))
 import numpy as np
 from srt_amd import render as R, _lib
