@@ -6,7 +6,9 @@
 // L2-resident table (2 MiB, so L1 misses and L2 hits, as the surface legs' loads mostly are).  Per case:
 //   A  lanes active (lane < A; the rest masked off by the branch),
 //   D  distinct lines per instruction (lane l reads line h(l % D), record (l / D) & 1 of its two),
-// and the time per load instruction per CU (all CUs busy: 8 waves per SIMD).
+// and the time per load instruction per CU (all CUs busy: 8 waves per SIMD).  Grouped cases (G > 1): the
+// lanes of each group of G read G consecutive 16-B pieces of one random record per instruction (a
+// cooperative load: G lanes fetch one lane's record together, then exchange within the group).
 //
 // build: hipcc -O3 --offload-arch=gfx950 -o tools/probes/vmem_cost tools/probes/vmem_cost.hip
 #include <hip/hip_runtime.h>
@@ -35,7 +37,18 @@ __global__ __launch_bounds__(256) void gather_kernel(const uint4* __restrict__ t
   const int lane = threadIdx.x & 63;
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   uint32_t acc = 0;
-  if (lane < A) {
+  if (D < 0 && lane < A) {  // grouped: G = -D lanes read one record's consecutive pieces per instruction
+    const int G = -D;
+    const uint32_t grp = (uint32_t)(lane / G), piece = (uint32_t)(lane % G);
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // 4 instructions, each a different record of the group
+        const uint32_t line = mix32(wave * 0x9E3779B9u + (uint32_t)(4 * it + k) * 0x85EBCA6Bu + grp * 0xC2B2AE35u) % n_lines;
+        const uint4 a = t[(size_t)line * 8 + piece];
+        acc ^= a.x ^ (a.y + a.z + a.w);
+      }
+    }
+  } else if (lane < A) {
     const uint32_t grp = (uint32_t)(lane % D), rec = (uint32_t)((lane / D) & 1);
     for (int it = 0; it < iters; ++it) {
       const uint32_t line = mix32(wave * 0x9E3779B9u + (uint32_t)it * 0x85EBCA6Bu + grp * 0xC2B2AE35u) % n_lines;
@@ -59,7 +72,8 @@ int main(int argc, char** argv) {
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const int blocks = cus * 8;  // 256-lane blocks: 8 waves per SIMD
   const int iters = 2000;
-  const int cases[][2] = {{64, 64}, {48, 48}, {32, 32}, {16, 16}, {8, 8}, {64, 32}, {64, 16}, {64, 8}, {32, 16}, {32, 8}};
+  const int cases[][2] = {{64, 64}, {48, 48}, {32, 32}, {16, 16}, {8, 8}, {64, 32}, {64, 16}, {64, 8}, {32, 16}, {32, 8},
+                          {64, -2}, {64, -4}, {64, -8}, {32, -4}, {32, -8}};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -81,8 +95,9 @@ int main(int argc, char** argv) {
     }
     const double instr_per_cu = (double)blocks * 4 * iters * 4 / cus;  // waves x iterations x 4 loads
     const double ns = best * 1e6 / instr_per_cu;
-    std::printf("  {\"active_lanes\": %d, \"lines_per_instr\": %d, \"ms\": %.3f, \"ns_per_load_instr_per_cu\": %.4f, "
-                "\"cycles_at_2p4GHz\": %.2f}%s\n", A, D, best, ns, ns * 2.4, k + 1 < n ? "," : "");
+    std::printf("  {\"active_lanes\": %d, \"%s\": %d, \"ms\": %.3f, \"ns_per_load_instr_per_cu\": %.4f, "
+                "\"cycles_at_2p4GHz\": %.2f}%s\n", A, D < 0 ? "lanes_per_record_group" : "lines_per_instr",
+                D < 0 ? -D : D, best, ns, ns * 2.4, k + 1 < n ? "," : "");
   }
   std::printf("]}\n");
   return 0;
