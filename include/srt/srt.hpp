@@ -311,6 +311,17 @@ class Model {
   Model(const Model&) = delete;
   Model& operator=(const Model&) = delete;
   srt_model* handle() const { return m_; }
+  // The BVH's primitive permutation (bvh.h:66-72): model_bvh.GetPrims()[i] is the loader's all_triangles[
+  // PrimOrder()[i]] (model_loader.cpp:299-331).  A closest hit (UpdateRaysAndTrace) is a GetPrims() index, as
+  // the shader's Intersects returns it; PrimOrder() maps it to the loader's order, in which
+  // BVH_intergration_tests.cpp:94 states its expected triangle.
+  std::vector<uint32_t> PrimOrder() const {
+    uint32_t sizes[4];
+    check(srt_model_sizes(m_, sizes), "Model::PrimOrder");
+    std::vector<uint32_t> order(sizes[1]);
+    check(srt_model_prim_order(m_, order.data()), "Model::PrimOrder");
+    return order;
+  }
 
  private:
   srt_model* m_;
