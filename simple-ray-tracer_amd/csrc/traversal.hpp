@@ -389,6 +389,9 @@ constexpr uint32_t kNodePad = 2;          // zero node records past the array: t
 // they hide (5,676 -> 5,239 Mrays/s on Rubik 1080p).
 template <bool LDSM>
 constexpr bool kSpine = SRT_SPINE && !LDSM;
+#ifndef SRT_MASK_LEAF2
+#define SRT_MASK_LEAF2 0
+#endif
 // Global-scene mode, fused schedule (trav_fused): sub-steps per traversal iteration
 #ifndef SRT_GLOBAL_FUSED
 #define SRT_GLOBAL_FUSED 8
@@ -674,11 +677,24 @@ __device__ __forceinline__ void trav_fused(const KParams& kp, const Lane& ln, Co
       x[0] = p[0];
       x[1] = p[1];
       x[2] = p[2];
+#if SRT_MASK_LEAF2
+      // experiment: a one-triangle leaf's lanes sit out its second record's three loads (a masked lane
+      // costs the vector-memory pipeline nothing, tools/probes/vmem_cost.hip); the record's stand-in is a
+      // zero record (a = 0: tested, then discarded by trav_leaf_x's k < n; a constant, so no load waits on it)
+      const bool two = at_leaf && t.cnt >= 2u;
+      x[3] = x[4] = x[5] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (at_int | two) x[3] = p[3];
+      if (spine | two) {
+        x[4] = p[4];
+        x[5] = p[5];
+      }
+#else
       x[3] = p[3];
       if (at_leaf | spine) {
         x[4] = p[4];
         x[5] = p[5];
       }
+#endif
       if (spine) {
         x[6] = p[6];
         x[7] = p[7];
