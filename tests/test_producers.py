@@ -72,6 +72,29 @@ def test_two_model_rebasing():
     _compare_scene(S.Scene.from_models([S.load_obj(RUBIK), S.load_obj(RUBIK)]), _scene_from_ref([m1, m2]))
 
 
+def test_primitive_permutation_across_models():
+    """srt_model_prim_order / srt_scene_tri_order: the BVH's permutation (bvh.h:66-72) of each model, offset by
+    the model's triangles before it in the flattened scene.  Checked against oracle/scene_ref.py's restatement
+    of the builder, and against the loader's per-corner vertex duplication (model_loader.cpp:302-331: loader
+    triangle k owns vertices 3k..3k+2, so a BVH-order triangle's first vertex is 3 x its input index), for
+    two OBJ models and a raw-triangle model (the parallel builder's size, serial and on 8 threads)."""
+    from srt_amd import render as RD
+
+    rub = S.load_obj(RUBIK)
+    soup = S.model_from_triangles(RD.synthetic_triangles(70_000, seed=5))
+    sc = S.Scene.from_models([rub, soup, rub])
+    n_r = rub.info()["triangles"]
+    n_s = soup.info()["triangles"]
+    order_r, order_s = rub.prim_order(), soup.prim_order()
+    assert sorted(order_r.tolist()) == list(range(n_r)) and sorted(order_s.tolist()) == list(range(n_s))
+    want = np.concatenate([order_r, order_s + n_r, order_r + n_r + n_s]).astype(np.uint32)
+    assert (sc.tri_input == want).all()
+    assert (sc.tris["v"][:, 0] == 3 * sc.tri_input).all()  # every model duplicates vertices per corner
+    packed, tris, _, _ = R.load_obj(RUBIK)
+    _, _, _, idx = R.build_bvh(packed, tris, with_order=True)
+    assert (np.asarray(idx, np.uint32) == order_r).all()
+
+
 def test_null_model_raises():
     with pytest.raises(Exception):
         S.Scene.from_models([None])
