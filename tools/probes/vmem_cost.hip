@@ -60,6 +60,31 @@ __global__ __launch_bounds__(256) void gather_kernel(const uint4* __restrict__ t
   if (acc == 0x12345678u) out[0] = acc;  // keeps the loads live
 }
 
+// per lane one random 16-B, 8-B or 4-B piece per instruction (W = 4, 2 or 1 dwords), all 64 lanes divergent
+template <int W>
+__global__ __launch_bounds__(256) void width_kernel(const uint32_t* __restrict__ t, uint32_t n_lines, int iters,
+                                                    uint32_t* out) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t acc = 0;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t line = mix32(gid * 0x9E3779B9u + (uint32_t)(4 * it + k) * 0x85EBCA6Bu) % n_lines;
+      const uint32_t* p = t + (size_t)line * 32;
+      if constexpr (W == 4) {
+        const uint4 v = *reinterpret_cast<const uint4*>(p);
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+      } else if constexpr (W == 2) {
+        const uint2 v = *reinterpret_cast<const uint2*>(p);
+        acc ^= v.x ^ v.y;
+      } else {
+        acc ^= *p;
+      }
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main(int argc, char** argv) {
   const size_t bytes = 2u << 20;
   const uint32_t n_lines = (uint32_t)(bytes / 128);
@@ -98,6 +123,25 @@ int main(int argc, char** argv) {
     std::printf("  {\"active_lanes\": %d, \"%s\": %d, \"ms\": %.3f, \"ns_per_load_instr_per_cu\": %.4f, "
                 "\"cycles_at_2p4GHz\": %.2f}%s\n", A, D < 0 ? "lanes_per_record_group" : "lines_per_instr",
                 D < 0 ? -D : D, best, ns, ns * 2.4, k + 1 < n ? "," : "");
+  }
+  std::printf("], \"widths\": [\n");
+  for (int W : {4, 2, 1}) {
+    float best = 1e30f;
+    for (int rep = 0; rep < 3; ++rep) {
+      CK(hipEventRecord(e0));
+      if (W == 4) hipLaunchKernelGGL(width_kernel<4>, dim3(blocks), dim3(256), 0, 0, (const uint32_t*)t, n_lines, iters, out);
+      else if (W == 2) hipLaunchKernelGGL(width_kernel<2>, dim3(blocks), dim3(256), 0, 0, (const uint32_t*)t, n_lines, iters, out);
+      else hipLaunchKernelGGL(width_kernel<1>, dim3(blocks), dim3(256), 0, 0, (const uint32_t*)t, n_lines, iters, out);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      best = ms < best ? ms : best;
+    }
+    const double instr_per_cu = (double)blocks * 4 * iters * 4 / cus;
+    const double ns = best * 1e6 / instr_per_cu;
+    std::printf("  {\"dwords_per_lane\": %d, \"active_lanes\": 64, \"ms\": %.3f, \"cycles_at_2p4GHz\": %.2f}%s\n", W, best,
+                ns * 2.4, W != 1 ? "," : "");
   }
   std::printf("]}\n");
   return 0;
