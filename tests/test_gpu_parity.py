@@ -114,6 +114,23 @@ def test_lights_edge_cases(rubik):
     assert_parity(none, 2)
 
 
+@pytest.mark.parametrize("scene", ["rubik", "knot", "spheres"])
+def test_many_lights_read_from_hbm(rubik, scene):
+    """300 point lights (9.6 KB of records, past the 8-KB LDS cap: shading reads them from HBM, kp.lights_lds
+    = 0) through SampleLights' RIS loop of 300 iterations (raytrace_compute.glsl:179-206), whose
+    randLightIndex = round(u * lightCount) can reach lightCount, one past the records (the zero light, as an
+    SSBO read past its end returns): the LDS kernel (Rubik), the fused 5-wave global instance (the knot) and
+    the sphere kernel match the oracle."""
+    rng = np.random.default_rng(300)
+    lights = [S.PointLight(tuple(rng.uniform((-12, 0, -12), (12, 22, 20)).astype(np.float32)),
+                           tuple(rng.uniform(0.1, 1.0, 3).astype(np.float32)), float(np.float32(rng.uniform(1, 40))))
+              for _ in range(300)]
+    models = {"rubik": [rubik], "knot": [R.torus_knot_model()], "spheres": None}[scene]
+    setup = R.make_setup(32, 24, show_model=scene != "spheres", models=models, lights=lights)
+    assert len(setup.lights) == 300
+    assert_parity(setup, 2)
+
+
 def test_ghost_bvh_count(rubik):
     """src/main.cpp:683 sets bvh_count = 2 with one model: bvhs[1] is an out-of-bounds (zero) record."""
     setup = R.make_setup(40, 32, show_model=True, models=[rubik], bvh_count=2)
