@@ -171,7 +171,7 @@ int srt_local_rows(srt_context* ctx);
  *   "launch.top_f4"      the top region its global-scene launch copied (0: none: the region did not fit
  *                        beside the rings and the light and material records);
  *   "launch.blocks_per_cu", "launch.block"  resident blocks per CU and lanes per block of its last
- *                        sample launch;
+ *                        sample_kernel, sphere_kernel or pool_kernel launch (0 after a wavefront-mode render);
  *   "launch.mats_lds"    1 when that launch read the material records from LDS (0: from HBM, where they
  *                        did not fit the LDS its blocks may take). */
 int srt_device(srt_context* ctx);

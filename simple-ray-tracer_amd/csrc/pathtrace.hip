@@ -597,6 +597,8 @@ int LaunchSpheres(srt_context* c, srt::KParams kp, size_t lds) {
   // resident blocks per CU: as many as its registers allow (C2 on one box, ms per launch: 3 blocks 3.23,
   // 4 3.00, 5 2.93; while the launch counter's atomic rate bound it, round 3, 3 were best)
   const int blocks = c->num_cus * std::min(per_cu, c->sphere_blocks);
+  c->launch_per_cu = std::min(per_cu, c->sphere_blocks);
+  c->launch_block = 256;
   {
     const long long waves = (long long)blocks * 4;
     const long long n_batches = (long long)((kp.W + 7) >> 3) * ((kp.local_rows + 7) >> 3) * kp.nframes;
@@ -633,6 +635,8 @@ int LaunchMode(srt_context* c, const srt::KParams& kc, size_t lds, bool count, b
 template <bool COUNT>
 int LaunchPool(srt_context* c, srt::KParams kp, size_t lds) {
   const int blocks = c->num_cus;
+  c->launch_per_cu = 1;
+  c->launch_block = 1024;
   kp.tail_start = (int)std::max<long long>(
       0, (long long)((kp.W + 7) >> 3) * ((kp.local_rows + 7) >> 3) * kp.nframes -
              (long long)c->tail_claims * srt::kClaim * blocks * srt::kPoolTravWaves);
@@ -718,6 +722,7 @@ int WfTrace(srt_context* c, const srt::KParams& kp, const srt::KParams& kt, cons
 // live count of every 8th iteration one group late (a pinned copy and an event), so the stream stays
 // full; the few iterations issued past the end find empty queues and return at once.
 int LaunchWavefront(srt_context* c, srt::KParams kp, bool tex) {
+  c->launch_per_cu = c->launch_block = 0;  // (its stage kernels' grids differ: no single value)
   constexpr int kMaxIters = 1 << 16;
   const uint32_t P = c->wf_slots;
   if (P > c->wf_cap) {

@@ -329,6 +329,25 @@ def test_top_levels_in_lds(monkeypatch, depth):
     assert_parity(two, 2)
 
 
+def test_launch_occupancy_reported(rubik):
+    """srt_get_int's launch.block / launch.blocks_per_cu report each kernel's resident occupancy: the LDS
+    kernel one 1024-lane block per CU (4 waves per SIMD), the fused global instance of a small tree five
+    256-lane blocks (5 waves), of a 1 M-triangle soup four (4 waves), the sphere kernel five."""
+    cases = [(R.make_setup(32, 24, show_model=True, models=[rubik]), 1024, 1),
+             (R.make_setup(32, 24, show_model=True, models=[R.torus_knot_model()]), 256, 5),
+             (R.make_setup(32, 24, show_model=True, models=[R.synthetic_model(1_000_000)]), 256, 4),
+             (R.make_setup(32, 24, show_model=False), 256, 5)]
+    for setup, block, per_cu in cases:
+        r = R.Renderer(setup)
+        try:
+            r.render(1)
+            r.finish()
+            got = (r.compute.GetInt("launch.block"), r.compute.GetInt("launch.blocks_per_cu"))
+        finally:
+            r.close()
+        assert got == (block, per_cu), (got, block, per_cu)
+
+
 @pytest.mark.parametrize("n_mats,mats_in_lds", [(1, True), (100, True), (150, True), (200, False), (600, False)])
 def test_top_region_keeps_occupancy_with_many_materials(n_mats, mats_in_lds):
     """the top levels' LDS region is sized beside the rings and the launch's light records, and
