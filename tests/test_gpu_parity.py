@@ -150,6 +150,92 @@ def test_two_models_with_transform(rubik):
     assert_parity(setup, 2)
 
 
+def _coincident_obj(tmp_path):
+    """A floor (y = 0) and a back wall (z = -6), each a 4x4 grid of quads written three times: 'red' and 'green'
+    are the same triangles (identical centroids, so the midpoint split keeps each twin pair in one leaf), 'blue'
+    is the grid shifted by half a cell inside the same plane (coplanar overlaps in other leaves).  Every hit on
+    them is a distance tie that only the visit order settles: `t < intersection_distance` is strict
+    (ray_intersects.glsl:89), so the first triangle the reference's traversal reaches keeps the hit."""
+    (tmp_path / "m.mtl").write_text("newmtl red\nKd 0.9 0.1 0.1\nKs 0.2 0.2 0.2\nNs 20\n"
+                                    "newmtl green\nKd 0.1 0.9 0.1\nKs 0.5 0.5 0.5\nNs 80\n"
+                                    "newmtl blue\nKd 0.1 0.1 0.9\nKs 0.05 0.05 0.05\nNs 5\n")
+    lines, nv = ["mtllib m.mtl"], 0
+
+    def grid(corner, du, dv, n=4):
+        nonlocal nv
+        base = nv
+        for j in range(n + 1):
+            for i in range(n + 1):
+                p = np.asarray(corner, np.float64) + i * np.asarray(du) + j * np.asarray(dv)
+                lines.append("v %.6g %.6g %.6g" % tuple(p))
+                nv += 1
+        return [(base + j * (n + 1) + i + 1, base + j * (n + 1) + i + 2, base + (j + 1) * (n + 1) + i + 2,
+                 base + (j + 1) * (n + 1) + i + 1) for j in range(n) for i in range(n)]
+
+    floor = grid((-8, 0, -8), (4, 0, 0), (0, 0, 4))
+    wall = grid((-8, 0, -6), (4, 0, 0), (0, 3.5, 0))
+    floor_b = grid((-6, 0, -6), (4, 0, 0), (0, 0, 4))
+    wall_b = grid((-6, 1.75, -6), (4, 0, 0), (0, 3.5, 0))
+    for mtl, quads in (("red", floor + wall), ("green", floor + wall), ("blue", floor_b + wall_b)):
+        lines.append("usemtl " + mtl)
+        lines += ["f %d %d %d %d" % q for q in quads]
+    (tmp_path / "m.obj").write_text("\n".join(lines) + "\n")
+    return tmp_path / "m.obj"
+
+
+@pytest.mark.parametrize("mode", ["lds", "global"])
+def test_coincident_triangles_keep_the_first_visited(tmp_path, monkeypatch, mode):
+    """Distance ties decided by visit order, in the renderer (both scene modes, counting and timed instances)
+    and in srt_trace_closest: identical twin triangles in one leaf, coplanar overlaps across leaves, and shadow
+    rays leaving the plane they start on.  The oracle's order is the reference's (ray_intersects.glsl:99-133),
+    so any reordering of a leaf's triangles or of sibling visits shows up as another material's colour."""
+    if mode == "global":
+        monkeypatch.setenv("SRT_FORCE_GLOBAL_SCENE", "1")
+    model = S.load_obj(_coincident_obj(tmp_path))
+    setup = R.make_setup(64, 48, show_model=True, models=[model])
+    sc = setup.scene
+    assert len(sc.tris) == 3 * 2 * 32
+    assert_parity(setup, 3)
+
+    rng = np.random.default_rng(17)
+    n = 4096
+    rays = np.zeros(n, S.RAY_DTYPE)
+    rays["o"] = rng.uniform([-7, 0.5, -5], [7, 12, 6], size=(n, 3)).astype(np.float32)
+    tgt = np.where((np.arange(n) % 2 == 0)[:, None],
+                   np.stack([rng.uniform(-7, 7, n), np.zeros(n), rng.uniform(-7, 7, n)], 1),     # the floor
+                   np.stack([rng.uniform(-7, 7, n), rng.uniform(0, 13, n), np.full(n, -6.0)], 1))  # the wall
+    rays["d"] = (tgt - rays["o"]).astype(np.float32)
+    rays["t"] = np.float32(1e30)
+    hits_o, t_o, _, _ = O.Oracle(sc).trace_closest(1, rays)
+    c = S.Compute().Init()
+    try:
+        c.bind_scene(sc)
+        c.SetUInt("bvh_count", 1)
+        hits, t = c.trace_closest(rays)
+    finally:
+        c.close()
+    assert (hits == hits_o).all() and bits_equal(t, t_o).all()
+    hit = hits != 0xFFFFFFFF
+    assert hit.mean() > 0.95
+    # a hit on a red or green triangle is a tie by construction (its twin computes the same t bit for bit)
+    twins = _twin_index(sc)
+    assert (twins[hits[hit]] >= 0).mean() > 0.3
+
+
+def _twin_index(sc):
+    """Per triangle, the index of the other triangle with the same three corners (-1 if none)."""
+    corners = sc.verts["pos"][sc.tris["v"]].reshape(len(sc.tris), 9)
+    out = np.full(len(sc.tris), -1, np.int64)
+    seen = {}
+    for i, row in enumerate(corners):
+        k = row.tobytes()
+        if k in seen:
+            out[i], out[seen[k]] = seen[k], i
+        else:
+            seen[k] = i
+    return out
+
+
 def test_textured_material_albedo(tmp_path):
     import test_producers as P
 
