@@ -510,8 +510,20 @@ constexpr int kGw5Block = SRT_GW5_BLOCK;
 static_assert(kGw5Block % 64 == 0 && 1280 % kGw5Block == 0, "SRT_GW5_BLOCK: 64-lane waves, 1280 lanes per CU");
 // Lanes per block of a global-scene launch of `gw` waves per SIMD (timed fused instance or not)
 constexpr int GlobalBlock(bool timed_fused, int gw) { return (timed_fused && gw == 5) ? kGw5Block : 256; }
-// The LDS one such block may take: its share of the CU's 160 KiB at gw waves per SIMD (4 SIMDs x 64 lanes)
-constexpr size_t GlobalBlockLds(int block, int gw) { return kLdsBytes * (size_t)block / ((size_t)gw * 256); }
+// gfx950 hands a block its LDS in units of 1/128 of the CU's 160 KiB (1,280 B), so n blocks run together
+// only when each asks at most floor(128 / n) units: 5 blocks fit at 32,000 B each, not at 32,001, while
+// hipOccupancyMaxActiveBlocksPerMultiprocessor still answers 5 up to 32,768 (and 3, 6, 7 likewise past their
+// limits; tools/probes/lds_fit.hip, profiles/r06_experiments/lds_fit.json).  The blocks per CU a launch's LDS
+// size allows:
+constexpr size_t kLdsGran = kLdsBytes / 128;
+constexpr int LdsBlocksPerCu(size_t lds) { return lds == 0 ? 1 << 30 : (int)(128 / ((lds + kLdsGran - 1) / kLdsGran)); }
+// The occupancy API's resident blocks per CU, capped by that allocation rule
+static int ResidentPerCu(int api_per_cu, size_t lds) { return std::max(1, std::min(api_per_cu, LdsBlocksPerCu(lds))); }
+// The LDS one such block may take: its whole units of the CU's 160 KiB at gw waves per SIMD (4 SIMDs x 64
+// lanes, gw * 256 / block blocks per CU)
+constexpr size_t GlobalBlockLds(int block, int gw) { return (128 / ((size_t)gw * 256 / (size_t)block)) * kLdsGran; }
+static_assert(GlobalBlockLds(256, 5) == 32000 && GlobalBlockLds(256, 4) == 40960 && GlobalBlockLds(640, 5) == 81920,
+              "the LDS shares the probe measured");
 
 template <bool COUNT, bool LDSM, bool PACK, int BLOCK, bool TEX, bool FUSE = false, int GW = 4>
 int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
@@ -524,7 +536,7 @@ int LaunchSamples(srt_context* c, srt::KParams kp, size_t lds) {
   if (per_cu == 0) {
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sample_kernel<COUNT, LDSM, PACK, BLOCK, TEX, FUSE, GW>,
                                                           BLOCK, lds));
-    per_cu = std::max(per_cu, 1);
+    per_cu = ResidentPerCu(per_cu, lds);
     c->occupancy.push_back({fn, lds, per_cu});
   }
   const int blocks = c->num_cus * per_cu;
@@ -591,7 +603,7 @@ int LaunchSpheres(srt_context* c, srt::KParams kp, size_t lds) {
     if (e.fn == fn && e.lds == lds) per_cu = e.per_cu;
   if (per_cu == 0) {
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, srt::sphere_kernel<COUNT>, 256, lds));
-    per_cu = std::max(per_cu, 1);
+    per_cu = ResidentPerCu(per_cu, lds);
     c->occupancy.push_back({fn, lds, per_cu});
   }
   // resident blocks per CU: as many as its registers allow (C2 on one box, ms per launch: 3 blocks 3.23,
@@ -657,7 +669,7 @@ int Resident(srt_context* c, F* fn, size_t lds, int* blocks) {
     if (e.fn == key && e.lds == lds) per_cu = e.per_cu;
   if (per_cu == 0) {
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds));
-    per_cu = std::max(per_cu, 1);
+    per_cu = ResidentPerCu(per_cu, lds);
     c->occupancy.push_back({key, lds, per_cu});
   }
   *blocks = c->num_cus * per_cu;
