@@ -172,6 +172,8 @@ int srt_local_rows(srt_context* ctx);
  *                        beside the rings and the light and material records);
  *   "launch.blocks_per_cu", "launch.block"  resident blocks per CU and lanes per block of its last
  *                        sample_kernel, sphere_kernel or pool_kernel launch (0 after a wavefront-mode render);
+ *                        the occupancy API's answer capped by gfx950's LDS allocation unit (1/128 of the
+ *                        CU's 160 KiB: n blocks run together only up to floor(128 / n) * 1,280 B each);
  *   "launch.mats_lds"    1 when that launch read the material records from LDS (0: from HBM, where they
  *                        did not fit the LDS its blocks may take). */
 int srt_device(srt_context* ctx);
