@@ -831,13 +831,45 @@ def test_save_image_matches_output(rubik, tmp_path):
 
 
 @pytest.mark.parametrize("yaw,pitch,origin", [(25.0, -12.0, (3.0, 12.0, 30.0)), (-70.0, 40.0, (-14.0, 6.0, 14.0)),
-                                              (180.0, -89.0, (0.5, 25.0, 0.25))])
+                                              (180.0, -89.0, (0.5, 25.0, 0.25)), (40.0, 10.0, (0.3, 4.0, 0.7))])
 def test_moved_camera_parity(rubik, yaw, pitch, origin):
     """Camera::Rotate / a moved origin (the reference's interactive path, camera.cpp:107-212): rays leave the
-    cube at grazing and inside-out angles, through the box faces the default camera never sees."""
+    cube at grazing and inside-out angles, through the box faces the default camera never sees; the last
+    camera sits inside the model's bounds, among the cubies, so every camera ray starts inside the root box
+    and IntersectsBox answers with its exit distance (ray_intersects.glsl:57), which then culls by it."""
     setup = R.make_setup(48, 40, show_model=True, models=[rubik])
     setup.camera.Rotate(yaw, pitch)
     setup.camera.position = np.asarray(origin, np.float32)
+    assert_parity(setup, 2)
+
+
+@pytest.mark.parametrize("mode", ["lds", "global"])
+def test_pathological_triangles(monkeypatch, mode):
+    """Triangles no exporter should write, inside a floor the camera sees: zero-area (collinear corners), a
+    point, a sliver 1e-6 wide, corners at +-1e30 (infinite edges and products in IntersectsTriangle), one
+    NaN corner (NaN bounds up the tree: the slab test's IEEE minNum/maxNum decide) and a huge triangle
+    spanning the scene.  The builder, both scene modes and the shading all take them; the frame is the
+    oracle's."""
+    if mode == "global":
+        monkeypatch.setenv("SRT_FORCE_GLOBAL_SCENE", "1")
+    rng = np.random.default_rng(41)
+    quads = []
+    for i in range(6):
+        for j in range(6):
+            x0, z0 = -12 + 4 * i, -12 + 4 * j
+            quads += [[x0, 0, z0, x0 + 4, 0, z0, x0 + 4, 0, z0 + 4], [x0, 0, z0, x0 + 4, 0, z0 + 4, x0, 0, z0 + 4]]
+    bad = [[-2, 3, -2, 0, 4, -1, 2, 5, 0],                     # collinear: zero area
+           [1, 6, 1, 1, 6, 1, 1, 6, 1],                        # a point
+           [-3, 2, 3, 3, 2, 3, 0, 2 + 1e-6, 3],                # a sliver
+           [0, 8, -4, 1e30, 8, -4, 0, 8, 1e30],                # infinite edges
+           [-1e30, 9, 0, 2, 9, 0, 0, -1e30, 1],
+           [4, 3, 4, 5, float("nan"), 4, 4, 4, 5],             # a NaN corner
+           [-40, 12, -40, 40, 14, -40, 0, 13, 40]]             # spans everything
+    bumps = rng.uniform(-8, 8, (40, 9)).astype(np.float32)
+    bumps[:, 1::3] = np.abs(bumps[:, 1::3]) * 0.5 + 1.0
+    xyz = np.concatenate([np.asarray(quads, np.float32), np.asarray(bad, np.float32), bumps])
+    model = S.model_from_triangles(xyz, kd=(0.7, 0.6, 0.5), ks=(0.3, 0.3, 0.3), ns=40.0)
+    setup = R.make_setup(48, 40, show_model=True, models=[model])
     assert_parity(setup, 2)
 
 
